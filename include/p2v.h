@@ -1,0 +1,140 @@
+/*
+ * p2v.h — C-ABI of libp2v, the MI355X-native batch Plonky2 verifier.
+ *
+ * This is the drop-in boundary for the reference's single entry point
+ *
+ *     verifyProof :: VerifierCircuitData -> ProofWithPublicInputs -> Bool
+ *                                              (reference src/Plonk/Verifier.hs:56-65)
+ *
+ * whose inputs are the Types.hs values decoded from JSON by the aeson instances
+ * (reference src/Types.hs:47-279, Gate strings via src/Gate/Parser.hs:27-242).
+ * The reference has no FFI; INTEGRATION.md shows the Haskell `foreign import ccall`
+ * binding (and the ctypes stub used by our Python mirror) for every entry point here.
+ *
+ * Conventions
+ *   - plain pointers + sizes only; no torch / HIP types in any signature
+ *   - functions return int: 0 = OK, < 0 = P2V_E_* (message via p2v_last_error_message())
+ *   - per-proof results are int8 status codes P2V_ACCEPT / P2V_REJECT / P2V_ERR_*
+ *     reproducing the reference's evaluation order:
+ *     Plonk identity -> PoW -> query rounds in order (initial Merkle, steps
+ *     (Merkle, eval, arity), final polynomial).
+ *   - the caller owns every buffer; the library owns opaque handles.
+ */
+#ifndef P2V_H
+#define P2V_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- per-proof status codes (int8) -------------------------------------------- */
+#define P2V_ACCEPT             1   /* verifyProof == True                                   */
+#define P2V_REJECT             0   /* verifyProof == False (Plonk identity, PoW, final poly) */
+#define P2V_ERR_INITIAL_MERKLE (-1) /* error "checkInitialTreeProofs: ... Merkle proof failed" Plonk/FRI.hs:108 */
+#define P2V_ERR_STEP_MERKLE    (-2) /* error "folding step Merkle proof does not check out"   Plonk/FRI.hs:310 */
+#define P2V_ERR_STEP_EVAL      (-3) /* error "folding step evaluation does not match ..."      Plonk/FRI.hs:311 */
+#define P2V_ERR_STEP_ARITY     (-4) /* error "folding stpe: reduction strategy ..."            Plonk/FRI.hs:312 */
+#define P2V_ERR_SHAPE          (-5) /* a list-length / shape `error` (safeZip*, buildListOracle, caps)      */
+#define P2V_ERR_CIRCUIT        (-6) /* circuit-level `error` (unknown gate, selector tally, MinSize, ...)   */
+#define P2V_ERR_PARSE          (-7) /* JSON did not decode (aeson `decode` == Nothing)                      */
+
+/* ---- function return codes ---------------------------------------------------- */
+#define P2V_OK          0
+#define P2V_E_PARSE    (-1)
+#define P2V_E_CIRCUIT  (-2)
+#define P2V_E_SHAPE    (-3)
+#define P2V_E_ARG      (-4)
+#define P2V_E_DEVICE   (-5)
+#define P2V_E_NODEVICE (-6)
+
+typedef struct p2v_circuit  p2v_circuit;   /* parsed VerifierCircuitData (Types.hs:220-224)   */
+typedef struct p2v_verifier p2v_verifier;  /* per-device workspace bound to one circuit         */
+
+/* Shape summary of a circuit (all derived from CommonCircuitData). */
+typedef struct p2v_circuit_info {
+  int32_t degree_bits;        /* fri_params.degree_bits                          Types.hs:165 */
+  int32_t lde_bits;           /* degree_bits + rate_bits                         Types.hs:165-167 */
+  int32_t cap_height;
+  int32_t num_challenges;     /* r                                               */
+  int32_t num_query_rounds;   /* Q                                               */
+  int32_t num_fri_steps;      /* from the reduction strategy, Plonk/FRI.hs:337-354 */
+  int32_t final_poly_len;     /* coefficients (F^2) of the final polynomial      */
+  int32_t num_public_inputs;
+  int32_t num_openings_this;  /* F^2 values in the first FRI opening batch       */
+  int32_t num_openings_next;  /* F^2 values in the second batch                   */
+  int32_t has_lookups;
+  int32_t num_gates;
+  int64_t proof_words;        /* u64 words of one packed proof                    */
+  int64_t trace_words;        /* u64 words of one debug trace (see p2v_trace_layout) */
+  int32_t oracle_widths[4];   /* leaf widths of the 4 initial oracles  Plonk/FRI.hs:56-65 */
+  int32_t step_arity_bits[8];
+} p2v_circuit_info;
+
+/* ---- circuits (host-only, no GPU needed) --------------------------------------- */
+int  p2v_circuit_from_json(const char* common_json, size_t common_len,
+                           const char* vkey_json,   size_t vkey_len,
+                           p2v_circuit** out);
+void p2v_circuit_free(p2v_circuit* c);
+int  p2v_circuit_get_info(const p2v_circuit* c, p2v_circuit_info* info);
+
+/* Pack one ProofWithPublicInputs JSON (Types.hs:245-254) into the circuit's fixed
+ * layout: dst must hold info.proof_words u64.  Field elements are canonicalised mod p
+ * (Goldilocks.hs:101-102).  Returns P2V_E_PARSE on bad JSON, P2V_E_SHAPE when a list
+ * length differs from what the circuit implies (the reference would raise a shape
+ * `error` or mis-verify on such input). */
+int  p2v_pack_proof_json(const p2v_circuit* c, const char* proof_json, size_t len, uint64_t* dst);
+
+/* ---- verification (GPU) ------------------------------------------------------------ */
+#define P2V_FLAG_INPUT_DEVICE  1u  /* `proofs` is a device pointer on the verifier's device  */
+#define P2V_FLAG_RESULT_DEVICE 2u  /* `results` (and trace) are device pointers              */
+#define P2V_FLAG_NO_SYNC       4u  /* do not synchronise the stream before returning          */
+
+int  p2v_device_count(void);
+
+/* Create a verifier on `device` able to take batches up to max_batch proofs.  All device
+ * memory is allocated here, none in p2v_verifier_run (graph-capturable). */
+int  p2v_verifier_create(const p2v_circuit* c, int device, size_t max_batch, p2v_verifier** out);
+void p2v_verifier_free(p2v_verifier* v);
+
+/* Verify n packed proofs (n * proof_words u64, proof-major).  results[i] gets the status
+ * of proof i.  trace (optional, may be NULL) receives n * trace_words u64 of intermediates
+ * for parity checks.  stream: a hipStream_t cast to void* (NULL = the default stream). */
+int  p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n,
+                      int8_t* results, uint64_t* trace, void* stream, uint32_t flags);
+
+/* One-shot convenience: create a verifier on `device`, verify, free. */
+int  p2v_verify_batch(const p2v_circuit* c, const uint64_t* proofs, size_t n,
+                      int8_t* results, int device);
+
+/* Per-launch timing of the last run (milliseconds, from HIP events on the run's stream):
+ * out[k] for kernel k in the order named by p2v_kernel_names(). Returns count. */
+int  p2v_verifier_last_timings(const p2v_verifier* v, float* out, int max);
+const char* p2v_kernel_names(void);   /* comma-separated */
+
+const char* p2v_last_error_message(void);
+const char* p2v_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+/* ---- debug trace layout (u64 words per proof), shared by the oracle --------------
+ *   off_pi_hash      4
+ *   off_betas        r          off_gammas   r          off_alphas  r
+ *   off_deltas       4r   (zero when the circuit has no lookups)
+ *   off_zeta         2          off_fri_alpha 2
+ *   off_fri_betas    2S         off_pow_response 1       off_query_idx Q
+ *   off_combined     2r   C_i(zeta) after alpha-combination  Plonk/Vanishing.hs:48-56
+ *   off_quotient     2r   sum_k zeta^(nk) q_{i,k}            Plonk/Verifier.hs:43-47
+ *   off_q_initial    2Q   combineInitial per query          Plonk/FRI.hs:151-207
+ *   off_q_folded     2Q   value after the last folding step Plonk/FRI.hs:306-323
+ *   off_q_final      2Q   final polynomial at x_final       Plonk/FRI.hs:325-327
+ *   off_flags        1    bit0 eqs_ok, bit1 pow_ok
+ * total = 4 + 3r + 4r + 4 + 2S + 1 + Q + 4r + 6Q + 1
+ */
+#define P2V_TRACE_WORDS(r, S, Q) (4 + 3*(r) + 4*(r) + 4 + 2*(S) + 1 + (Q) + 4*(r) + 6*(Q) + 1)
+
+#endif /* P2V_H */

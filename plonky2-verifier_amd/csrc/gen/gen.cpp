@@ -1,0 +1,628 @@
+// gen.cpp — synthetic valid-proof generator (workload + fixture source, NOT part of the
+// verifier path).  A degenerate-circuit Plonky2 prover:
+//
+//   * every gate-selector constant column is the constant UNUSED = 2^32-1 and there are
+//     >= 2 selector groups, so every gate filter (Gate/Selector.hs:83-89) is 0 at zeta;
+//   * lookup-selector columns are 0 (every lookup term carries a selector, Lookups.hs:78-132);
+//   * sigma_j(X) = k_j X, so the permutation numerators equal the denominators
+//     (Vanishing.hs:99-111) with Z == partial products == 1;
+//   * quotient polynomials are 0.
+// Hence C(zeta) = 0 = Q(zeta)(zeta^n - 1) and the Plonk identity holds, while the verifier
+// still evaluates every gate program, lookup argument and the whole FRI proof.  Wires,
+// gate constants and lookup_zs are random polynomials of degree < n, so proofs differ.
+// The FRI part is a real prover: LDE on g*H in bit-reversed order, Merkle trees with caps,
+// openings at zeta / omega*zeta, the combined quotient codeword, arity-2^k folding with
+// commit-phase trees, final polynomial, proof-of-work grinding and query openings, all
+// following the verifier conventions of Plonk/FRI.hs and Challenge/*.hs.
+//
+// Exposed as a C ABI (libp2v_gen.so) for tests/ and bench.py.
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <cstdio>
+#include <string>
+#include <vector>
+#include <memory>
+#include <stdexcept>
+#include "../gl.h"
+#include "../poseidon.h"
+
+using gl::E;
+using u64 = uint64_t;
+
+namespace {
+
+// ------------------------------------------------------------------------ rng
+struct Rng {
+  u64 s;
+  explicit Rng(u64 seed) : s(seed ^ 0x9E3779B97F4A7C15ULL) {}
+  u64 next() {  // splitmix64
+    u64 z = (s += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+  }
+  u64 field() { for (;;) { u64 x = next(); if (x < gl::P) return x; } }
+};
+
+// ------------------------------------------------------------------ hashing
+void sponge(const u64* xs, size_t n, u64 out[4]) {
+  u64 st[12] = {0};
+  for (size_t i = 0; i < n; i += 8) {
+    size_t k = n - i < 8 ? n - i : 8;
+    for (size_t j = 0; j < k; j++) st[j] = xs[i + j];
+    p2::permute(st);
+  }
+  memcpy(out, st, 32);
+}
+void compress(const u64* a, const u64* b, u64 out[4]) {
+  u64 st[12] = {0};
+  memcpy(st, a, 32); memcpy(st + 4, b, 32);
+  p2::permute(st);
+  memcpy(out, st, 32);
+}
+
+struct Digest { u64 e[4]; };
+
+// Merkle tree over n = 2^lg leaves (leaf digests given), cap of 2^cap_h nodes.
+struct Tree {
+  int lg = 0, cap_h = 0;
+  std::vector<std::vector<Digest>> layers;   // layers[0] = leaf digests
+  void build(std::vector<Digest>&& leaves, int lg_, int cap_h_) {
+    lg = lg_; cap_h = cap_h_;
+    layers.clear(); layers.push_back(std::move(leaves));
+    for (int l = lg; l > cap_h; l--) {
+      const auto& prev = layers.back();
+      std::vector<Digest> nx(prev.size() / 2);
+      for (size_t i = 0; i < nx.size(); i++) compress(prev[2 * i].e, prev[2 * i + 1].e, nx[i].e);
+      layers.push_back(std::move(nx));
+    }
+  }
+  const std::vector<Digest>& cap() const { return layers.back(); }
+  std::vector<Digest> path(size_t idx) const {
+    std::vector<Digest> sib;
+    for (size_t l = 0; l + 1 < layers.size(); l++) { sib.push_back(layers[l][idx ^ 1]); idx >>= 1; }
+    return sib;
+  }
+};
+
+// ------------------------------------------------------------------ FFT
+// in-place radix-2 DIT FFT of size 2^lg with generator w (natural order in / out)
+void fft(std::vector<u64>& a, int lg, u64 w) {
+  size_t n = (size_t)1 << lg;
+  for (size_t i = 1, j = 0; i < n; i++) {
+    size_t bit = n >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j ^= bit;
+    if (i < j) std::swap(a[i], a[j]);
+  }
+  std::vector<u64> tw(n / 2);
+  for (size_t len = 2; len <= n; len <<= 1) {
+    u64 wl = w;
+    for (size_t t = len; t < n; t <<= 1) wl = gl::mul(wl, wl);   // w^(n/len)
+    tw[0] = 1;
+    for (size_t k = 1; k < len / 2; k++) tw[k] = gl::mul(tw[k - 1], wl);
+    for (size_t i = 0; i < n; i += len)
+      for (size_t k = 0; k < len / 2; k++) {
+        u64 u = a[i + k], v = gl::mul(a[i + k + len / 2], tw[k]);
+        a[i + k] = gl::add(u, v); a[i + k + len / 2] = gl::sub(u, v);
+      }
+  }
+}
+void efft(std::vector<E>& a, int lg, u64 w) {
+  std::vector<u64> re(a.size()), im(a.size());
+  for (size_t i = 0; i < a.size(); i++) { re[i] = a[i].a; im[i] = a[i].b; }
+  fft(re, lg, w); fft(im, lg, w);
+  for (size_t i = 0; i < a.size(); i++) a[i] = E{re[i], im[i]};
+}
+
+// LDE of a coefficient vector (length N) onto g*<eta> of size 2^lde, natural order
+std::vector<u64> lde(const std::vector<u64>& coeffs, int lde_bits) {
+  size_t M = (size_t)1 << lde_bits;
+  std::vector<u64> a(M, 0);
+  u64 gp = 1;
+  for (size_t k = 0; k < coeffs.size(); k++) { a[k] = gl::mul(coeffs[k], gp); gp = gl::mul(gp, gl::MULT_GEN); }
+  fft(a, lde_bits, gl::subgroup_gen(lde_bits));
+  return a;
+}
+
+E eval_at(const std::vector<u64>& coeffs, E x) {   // Horner, base coefficients at F^2 point
+  E acc = gl::e0();
+  for (size_t k = coeffs.size(); k-- > 0;) acc = gl::eadd(gl::emul(acc, x), gl::eb(coeffs[k]));
+  return acc;
+}
+
+void batch_inv(std::vector<E>& v) {   // Montgomery trick (no zeros expected)
+  size_t n = v.size();
+  std::vector<E> pre(n);
+  E acc = gl::eb(1);
+  for (size_t i = 0; i < n; i++) { pre[i] = acc; acc = gl::emul(acc, v[i]); }
+  E inv = gl::einv(acc);
+  for (size_t i = n; i-- > 0;) { E t = gl::emul(inv, pre[i]); inv = gl::emul(inv, v[i]); v[i] = t; }
+}
+
+// ------------------------------------------------------------------ duplex (Challenge/Pure.hs)
+struct Duplex {
+  u64 st[12] = {0};
+  bool absorbing = true;
+  u64 buf[8]; int nbuf = 0;
+  u64 out[8]; int nout = 0, pos = 0;
+  void dup() { for (int i = 0; i < nbuf; i++) st[i] = buf[i]; p2::permute(st); }
+  void fresh() { absorbing = false; for (int i = 0; i < 8; i++) out[i] = st[7 - i]; nout = 8; pos = 0; }
+  void absorb(u64 x) {
+    if (!absorbing) { absorbing = true; nbuf = 0; }
+    if (nbuf < 8) { buf[nbuf++] = x; return; }
+    dup(); nbuf = 0; buf[nbuf++] = x;
+  }
+  u64 squeeze() {
+    if (absorbing) { dup(); nbuf = 0; fresh(); }
+    else if (pos == nout) { p2::permute(st); fresh(); }
+    return out[pos++];
+  }
+  E squeeze_e() { E r; r.a = squeeze(); r.b = squeeze(); return r; }
+  void absorb_digests(const std::vector<Digest>& ds) { for (auto& d : ds) for (int i = 0; i < 4; i++) absorb(d.e[i]); }
+  void absorb_e(const std::vector<E>& v) { for (auto& x : v) { absorb(x.a); absorb(x.b); } }
+};
+
+// ------------------------------------------------------------------ JSON helpers
+struct J {
+  std::string s;
+  void raw(const char* t) { s += t; }
+  void u(u64 x) { char b[32]; snprintf(b, sizeof b, "%llu", (unsigned long long)x); s += b; }
+  void i(long long x) { char b[32]; snprintf(b, sizeof b, "%lld", x); s += b; }
+  void digest(const Digest& d) { raw("{\"elements\":["); for (int k = 0; k < 4; k++) { if (k) raw(","); u(d.e[k]); } raw("]}"); }
+  void cap(const std::vector<Digest>& c) { raw("["); for (size_t k = 0; k < c.size(); k++) { if (k) raw(","); digest(c[k]); } raw("]"); }
+  void fs(const u64* v, size_t n) { raw("["); for (size_t k = 0; k < n; k++) { if (k) raw(","); u(v[k]); } raw("]"); }
+  void es(const std::vector<E>& v) { raw("["); for (size_t k = 0; k < v.size(); k++) { if (k) raw(","); raw("["); u(v[k].a); raw(","); u(v[k].b); raw("]"); } raw("]"); }
+};
+
+// ------------------------------------------------------------------ circuit
+struct Circuit {
+  int degree_bits = 12, rate_bits = 3, cap_height = 4, pow_bits = 16, num_queries = 28;
+  int arity_bits = 4, final_poly_bits = 5;
+  int num_wires = 135, num_routed = 80, num_gate_consts = 2, r = 2, qdf = 8;
+  int num_pis = 4;
+  int ngroups = 3;
+  int nlp = 0;                 // num_lookup_polys (0 = no lookups)
+  std::vector<std::vector<std::pair<u64, u64>>> luts;
+  std::vector<std::string> gates;
+  std::vector<int> sel_idx;
+  std::vector<u64> k_is;
+  int npp = 9;                 // num_partial_products
+  int num_gate_constraints = 123;
+  u64 circuit_seed = 1;
+  // derived
+  int N = 0, lde_bits = 0, nls = 0, num_constants = 0;
+  std::vector<int> arities;
+  std::vector<std::vector<u64>> gate_const_coeffs;   // random polys
+  std::vector<u64> const_lde;                         // [M][85] bit-reversed rows of the constants oracle
+  int const_width = 0;
+  Tree const_tree;
+  Digest circuit_digest;
+  std::string common_json, vkey_json;
+};
+
+std::string coset_gate_string(int bits) {
+  // CosetInterpolationGate with barycentric weights of the subgroup (CosetInterp.hs:36-49)
+  int n = 1 << bits;
+  u64 g = gl::subgroup_gen(bits);
+  std::vector<u64> pts(n); pts[0] = 1; for (int i = 1; i < n; i++) pts[i] = gl::mul(pts[i - 1], g);
+  std::string w = "[";
+  for (int i = 0; i < n; i++) {
+    u64 prod = 1;
+    for (int j = 0; j < n; j++) if (j != i) prod = gl::mul(prod, gl::sub(pts[i], pts[j]));
+    if (i) w += ", ";
+    w += std::to_string((unsigned long long)gl::inv(prod));
+  }
+  w += "]";
+  int max_degree = 8;
+  int n_int_guess = (n - 2) / (max_degree - 1);
+  int degree = (n - 2) / (n_int_guess + 1) + 2;
+  return "CosetInterpolationGate { subgroup_bits: " + std::to_string(bits) + ", degree: " + std::to_string(degree) +
+         ", barycentric_weights: " + w + ", _phantom: PhantomData<plonky2_field::goldilocks_field::GoldilocksField> }<D=2>";
+}
+
+std::string keccak_str(u64 seed) {
+  Rng rg(seed); std::string s = "[";
+  for (int i = 0; i < 32; i++) { if (i) s += ", "; s += std::to_string((unsigned)(rg.next() & 255)); }
+  return s + "]";
+}
+
+void build_circuit(Circuit& C) {
+  C.N = 1 << C.degree_bits;
+  C.lde_bits = C.degree_bits + C.rate_bits;
+  C.nls = C.luts.empty() ? 0 : 4 + (int)C.luts.size();
+  C.num_constants = C.ngroups + C.nls + C.num_gate_consts;
+  C.npp = (C.num_routed + C.qdf - 1) / C.qdf - 1;
+  C.arities.clear();
+  for (int logn = C.degree_bits; logn > C.final_poly_bits; logn -= C.arity_bits) C.arities.push_back(C.arity_bits);
+  if (C.gates.empty()) {
+    C.gates = {
+      "NoopGate",
+      "ConstantGate { num_consts: 2 }",
+      "PoseidonMdsGate(PhantomData<plonky2_field::goldilocks_field::GoldilocksField>)<WIDTH=12>",
+      "PublicInputGate",
+      "BaseSumGate { num_limbs: 63 } + Base: 2",
+      "ReducingExtensionGate { num_coeffs: 32 }",
+      "ReducingGate { num_coeffs: 43 }",
+      "ArithmeticExtensionGate { num_ops: 10 }",
+      "ArithmeticGate { num_ops: 20 }",
+      "MulExtensionGate { num_ops: 13 }",
+      "RandomAccessGate { bits: 4, num_copies: 4, num_extra_constants: 2, _phantom: PhantomData<plonky2_field::goldilocks_field::GoldilocksField> }<D=2>",
+      "ExponentiationGate { num_power_bits: 66 }",
+      coset_gate_string(4),
+      "PoseidonGate(PhantomData<plonky2_field::goldilocks_field::GoldilocksField>)<WIDTH=12>",
+    };
+    if (!C.luts.empty()) {
+      for (size_t t = 0; t < C.luts.size(); t++) {
+        C.gates.insert(C.gates.begin() + 1, "LookupTableGate { num_slots: 26, lut_hash: " + keccak_str(100 + t) +
+                                               ", last_lut_row: " + std::to_string((C.luts[t].size() + 25) / 26) + " }");
+        C.gates.insert(C.gates.begin() + 1, "LookupGate { num_slots: 40, lut_hash: " + keccak_str(100 + t) + " }");
+      }
+    }
+  }
+  C.sel_idx.assign(C.gates.size(), 0);
+  {  // split gates into ngroups contiguous groups
+    size_t per = (C.gates.size() + C.ngroups - 1) / C.ngroups;
+    for (size_t g = 0; g < C.gates.size(); g++) C.sel_idx[g] = (int)(g / per);
+    C.ngroups = C.sel_idx.back() + 1;
+    C.num_constants = C.ngroups + C.nls + C.num_gate_consts;
+  }
+  C.k_is.resize(C.num_routed);
+  { u64 k = 1; for (int i = 0; i < C.num_routed; i++) { C.k_is[i] = k; k = gl::mul(k, gl::MULT_GEN); } }
+
+  Rng rg(C.circuit_seed * 7919 + 17);
+  C.gate_const_coeffs.assign(C.num_gate_consts, std::vector<u64>(C.N));
+  for (auto& p : C.gate_const_coeffs) for (auto& c : p) c = rg.field();
+  for (int i = 0; i < 4; i++) C.circuit_digest.e[i] = rg.field();
+
+  // constants oracle: [selectors (UNUSED) | lookup selectors (0) | gate constants | sigmas]
+  size_t M = (size_t)1 << C.lde_bits;
+  C.const_width = C.num_constants + C.num_routed;
+  C.const_lde.assign(M * C.const_width, 0);
+  std::vector<std::vector<u64>> gc_lde;
+  for (auto& p : C.gate_const_coeffs) gc_lde.push_back(lde(p, C.lde_bits));
+  u64 eta = gl::subgroup_gen(C.lde_bits);
+  std::vector<u64> xs(M); { u64 x = gl::MULT_GEN; for (size_t i = 0; i < M; i++) { xs[i] = x; x = gl::mul(x, eta); } }
+  for (size_t idx = 0; idx < M; idx++) {
+    size_t nat = gl::rev_bits(C.lde_bits, (uint32_t)idx);
+    u64* row = &C.const_lde[idx * C.const_width];
+    int c = 0;
+    for (int g = 0; g < C.ngroups; g++) row[c++] = 0xFFFFFFFFULL;
+    for (int g = 0; g < C.nls; g++) row[c++] = 0;
+    for (int g = 0; g < C.num_gate_consts; g++) row[c++] = gc_lde[g][nat];
+    for (int j = 0; j < C.num_routed; j++) row[c++] = gl::mul(C.k_is[j], xs[nat]);
+  }
+  std::vector<Digest> leaves(M);
+  for (size_t idx = 0; idx < M; idx++) sponge(&C.const_lde[idx * C.const_width], C.const_width, leaves[idx].e);
+  C.const_tree.build(std::move(leaves), C.lde_bits, C.cap_height);
+
+  // ---------------------------------------------------------- JSON (Types.hs field names)
+  J j;
+  auto fri_config = [&](J& o) {
+    o.raw("{\"rate_bits\":"); o.i(C.rate_bits); o.raw(",\"cap_height\":"); o.i(C.cap_height);
+    o.raw(",\"proof_of_work_bits\":"); o.i(C.pow_bits);
+    o.raw(",\"reduction_strategy\":{\"ConstantArityBits\":["); o.i(C.arity_bits); o.raw(","); o.i(C.final_poly_bits); o.raw("]}");
+    o.raw(",\"num_query_rounds\":"); o.i(C.num_queries); o.raw("}");
+  };
+  j.raw("{\"config\":{\"num_wires\":"); j.i(C.num_wires); j.raw(",\"num_routed_wires\":"); j.i(C.num_routed);
+  j.raw(",\"num_constants\":"); j.i(C.num_gate_consts); j.raw(",\"use_base_arithmetic_gate\":true,\"security_bits\":100");
+  j.raw(",\"num_challenges\":"); j.i(C.r); j.raw(",\"zero_knowledge\":false,\"randomize_unused_wires\":true");
+  j.raw(",\"max_quotient_degree_factor\":"); j.i(C.qdf); j.raw(",\"fri_config\":"); fri_config(j); j.raw("}");
+  j.raw(",\"fri_params\":{\"config\":"); fri_config(j); j.raw(",\"hiding\":false,\"degree_bits\":"); j.i(C.degree_bits);
+  j.raw(",\"reduction_arity_bits\":["); for (size_t k = 0; k < C.arities.size(); k++) { if (k) j.raw(","); j.i(C.arities[k]); } j.raw("]}");
+  j.raw(",\"gates\":[");
+  for (size_t g = 0; g < C.gates.size(); g++) { if (g) j.raw(","); j.raw("\""); j.raw(C.gates[g].c_str()); j.raw("\""); }
+  j.raw("],\"selectors_info\":{\"selector_indices\":[");
+  for (size_t g = 0; g < C.sel_idx.size(); g++) { if (g) j.raw(","); j.i(C.sel_idx[g]); }
+  j.raw("],\"groups\":[");
+  {
+    size_t per = (C.gates.size() + C.ngroups - 1) / C.ngroups;
+    for (int g = 0; g < C.ngroups; g++) {
+      if (g) j.raw(",");
+      size_t s = g * per, e = std::min(C.gates.size(), (size_t)(g + 1) * per);
+      j.raw("{\"start\":"); j.i((long long)s); j.raw(",\"end\":"); j.i((long long)e); j.raw("}");
+    }
+  }
+  j.raw("]},\"quotient_degree_factor\":"); j.i(C.qdf);
+  j.raw(",\"num_gate_constraints\":"); j.i(C.num_gate_constraints);
+  j.raw(",\"num_constants\":"); j.i(C.num_constants);
+  j.raw(",\"num_public_inputs\":"); j.i(C.num_pis);
+  j.raw(",\"k_is\":"); j.fs(C.k_is.data(), C.k_is.size());
+  j.raw(",\"num_partial_products\":"); j.i(C.npp);
+  j.raw(",\"num_lookup_polys\":"); j.i(C.nlp);
+  j.raw(",\"num_lookup_selectors\":"); j.i(C.nls);
+  j.raw(",\"luts\":[");
+  for (size_t t = 0; t < C.luts.size(); t++) {
+    if (t) j.raw(",");
+    j.raw("[");
+    for (size_t k = 0; k < C.luts[t].size(); k++) { if (k) j.raw(","); j.raw("["); j.u(C.luts[t][k].first); j.raw(","); j.u(C.luts[t][k].second); j.raw("]"); }
+    j.raw("]");
+  }
+  j.raw("]}");
+  C.common_json = std::move(j.s);
+  J v;
+  v.raw("{\"constants_sigmas_cap\":"); v.cap(C.const_tree.cap()); v.raw(",\"circuit_digest\":"); v.digest(C.circuit_digest); v.raw("}");
+  C.vkey_json = std::move(v.s);
+}
+
+// ------------------------------------------------------------------ witness (wires + zs/pp oracle)
+struct Witness {
+  std::vector<std::vector<u64>> wire_coeffs;     // [W][N]
+  std::vector<std::vector<u64>> lzs_coeffs;      // [r*nlp][N]
+  std::vector<u64> wires_lde;                    // [M][W] bit-reversed rows
+  std::vector<u64> zs_lde;                       // [M][r*(1+npp+nlp)]
+  std::vector<u64> q_lde;                        // [M][r*qdf] (all zero)
+  int zw = 0, qw = 0;
+  Tree wires_tree, zs_tree, q_tree;
+};
+
+Witness* make_witness(const Circuit& C, u64 seed) {
+  auto* W = new Witness();
+  Rng rg(seed * 1000003 + 11);
+  size_t M = (size_t)1 << C.lde_bits;
+  W->wire_coeffs.assign(C.num_wires, std::vector<u64>(C.N));
+  for (auto& p : W->wire_coeffs) for (auto& c : p) c = rg.field();
+  int nl = C.r * C.nlp;
+  W->lzs_coeffs.assign(nl, std::vector<u64>(C.N));
+  for (auto& p : W->lzs_coeffs) for (auto& c : p) c = rg.field();
+  W->wires_lde.assign(M * C.num_wires, 0);
+  for (int w = 0; w < C.num_wires; w++) {
+    auto l = lde(W->wire_coeffs[w], C.lde_bits);
+    for (size_t idx = 0; idx < M; idx++) W->wires_lde[idx * C.num_wires + w] = l[gl::rev_bits(C.lde_bits, (uint32_t)idx)];
+  }
+  // zs/pp oracle columns: [zs (r) | partial products (r*npp) | lookup zs (r*nlp)] — Z == pp == 1
+  W->zw = C.r * (1 + C.npp + C.nlp);
+  W->zs_lde.assign(M * W->zw, 1);
+  for (int k = 0; k < nl; k++) {
+    auto l = lde(W->lzs_coeffs[k], C.lde_bits);
+    int col = C.r * (1 + C.npp) + k;
+    for (size_t idx = 0; idx < M; idx++) W->zs_lde[idx * W->zw + col] = l[gl::rev_bits(C.lde_bits, (uint32_t)idx)];
+  }
+  W->qw = C.r * C.qdf;
+  W->q_lde.assign(M * W->qw, 0);
+  auto tree_of = [&](const std::vector<u64>& rows, int width, Tree& t) {
+    std::vector<Digest> leaves(M);
+    for (size_t idx = 0; idx < M; idx++) sponge(&rows[idx * width], width, leaves[idx].e);
+    t.build(std::move(leaves), C.lde_bits, C.cap_height);
+  };
+  tree_of(W->wires_lde, C.num_wires, W->wires_tree);
+  tree_of(W->zs_lde, W->zw, W->zs_tree);
+  tree_of(W->q_lde, W->qw, W->q_tree);
+  return W;
+}
+
+// ------------------------------------------------------------------ proof
+std::string make_proof(const Circuit& C, const Witness& W, u64 pi_seed) {
+  Rng rg(pi_seed * 104729 + 5);
+  const size_t M = (size_t)1 << C.lde_bits;
+  const int r = C.r;
+  std::vector<u64> pis(C.num_pis);
+  for (auto& x : pis) x = rg.field();
+  u64 pih[4]; sponge(pis.data(), pis.size(), pih);
+  if (pis.empty()) memset(pih, 0, sizeof pih);
+
+  Duplex d;
+  for (int i = 0; i < 4; i++) d.absorb(C.circuit_digest.e[i]);
+  for (int i = 0; i < 4; i++) d.absorb(pih[i]);
+  d.absorb_digests(W.wires_tree.cap());
+  std::vector<u64> betas(r), gammas(r);
+  for (auto& b : betas) b = d.squeeze();
+  for (auto& g : gammas) g = d.squeeze();
+  if (C.nlp > 0) for (int i = 0; i < 2 * r; i++) (void)d.squeeze();
+  d.absorb_digests(W.zs_tree.cap());
+  for (int i = 0; i < r; i++) (void)d.squeeze();   // alphas
+  d.absorb_digests(W.q_tree.cap());
+  E zeta = d.squeeze_e();
+  u64 omega = gl::subgroup_gen(C.degree_bits);
+  E zeta_w = gl::escale(omega, zeta);
+
+  // openings at zeta (OpeningSet order, Types.hs:265-279)
+  std::vector<E> o_const, o_sig, o_wires, o_zs, o_zs_next, o_pp, o_quot, o_lzs, o_lzs_next;
+  for (int g = 0; g < C.ngroups; g++) o_const.push_back(gl::eb(0xFFFFFFFFULL));
+  for (int g = 0; g < C.nls; g++) o_const.push_back(gl::e0());
+  for (int g = 0; g < C.num_gate_consts; g++) o_const.push_back(eval_at(C.gate_const_coeffs[g], zeta));
+  for (int j = 0; j < C.num_routed; j++) o_sig.push_back(gl::escale(C.k_is[j], zeta));
+  for (int w = 0; w < C.num_wires; w++) o_wires.push_back(eval_at(W.wire_coeffs[w], zeta));
+  for (int i = 0; i < r; i++) { o_zs.push_back(gl::eb(1)); o_zs_next.push_back(gl::eb(1)); }
+  for (int i = 0; i < r * C.npp; i++) o_pp.push_back(gl::eb(1));
+  for (int i = 0; i < r * C.qdf; i++) o_quot.push_back(gl::e0());
+  for (int k = 0; k < r * C.nlp; k++) { o_lzs.push_back(eval_at(W.lzs_coeffs[k], zeta)); o_lzs_next.push_back(eval_at(W.lzs_coeffs[k], zeta_w)); }
+  std::vector<E> b1, b2;
+  for (auto* v : {&o_const, &o_sig, &o_wires, &o_zs, &o_pp, &o_quot, &o_lzs}) b1.insert(b1.end(), v->begin(), v->end());
+  for (auto* v : {&o_zs_next, &o_lzs_next}) b2.insert(b2.end(), v->begin(), v->end());
+  d.absorb_e(b1); d.absorb_e(b2);
+  E alpha = d.squeeze_e();
+
+  // combined codeword at every LDE position (bit-reversed order), Plonk/FRI.hs:151-207
+  auto reduce = [&](const std::vector<E>& xs) { E acc = gl::e0(); for (size_t i = xs.size(); i-- > 0;) acc = gl::eadd(xs[i], gl::emul(alpha, acc)); return acc; };
+  E y0 = reduce(b1), y1 = reduce(b2);
+  int npp_all = (C.num_routed + C.qdf - 1) / C.qdf;   // zs + pps per challenge
+  int len2 = r + r * C.nlp;
+  E alpha_len2 = gl::epow(alpha, (u64)len2);
+  u64 eta = gl::subgroup_gen(C.lde_bits);
+  std::vector<E> den0(M), den1(M);
+  std::vector<u64> px(M);
+  for (size_t idx = 0; idx < M; idx++) {
+    px[idx] = gl::mul(gl::MULT_GEN, gl::pow(eta, gl::rev_bits(C.lde_bits, (uint32_t)idx)));
+    den0[idx] = gl::esub(gl::eb(px[idx]), zeta);
+    den1[idx] = gl::esub(gl::eb(px[idx]), zeta_w);
+  }
+  batch_inv(den0); batch_inv(den1);
+  std::vector<E> cw(M);
+  std::vector<u64> row;
+  for (size_t idx = 0; idx < M; idx++) {
+    // firstBatch = consts|sigmas | wires | pp-part (r*npp_all) | quotient | lookup part
+    const u64* rc = &C.const_lde[idx * C.const_width];
+    const u64* rw = &W.wires_lde[idx * C.num_wires];
+    const u64* rz = &W.zs_lde[idx * W.zw];
+    const u64* rq = &W.q_lde[idx * W.qw];
+    row.clear();
+    row.insert(row.end(), rc, rc + C.const_width);
+    row.insert(row.end(), rw, rw + C.num_wires);
+    row.insert(row.end(), rz, rz + r * npp_all);
+    row.insert(row.end(), rq, rq + W.qw);
+    row.insert(row.end(), rz + r * npp_all, rz + W.zw);
+    E g0 = gl::e0();
+    for (size_t i = row.size(); i-- > 0;) g0 = gl::eadd(gl::eb(row[i]), gl::emul(alpha, g0));
+    E g1 = gl::e0();
+    std::vector<u64> sb(rz, rz + r); sb.insert(sb.end(), rz + r * npp_all, rz + W.zw);
+    for (size_t i = sb.size(); i-- > 0;) g1 = gl::eadd(gl::eb(sb[i]), gl::emul(alpha, g1));
+    E one = gl::emul(gl::esub(g0, y0), den0[idx]);
+    E two = gl::emul(gl::esub(g1, y1), den1[idx]);
+    cw[idx] = gl::eadd(gl::emul(alpha_len2, one), two);
+  }
+
+  // commit phase (folding), Plonk/FRI.hs:233-323 conventions
+  std::vector<Tree> step_trees;
+  std::vector<std::vector<E>> layers;   // values of each layer (bit-reversed order)
+  std::vector<E> betas_fri;
+  layers.push_back(cw);
+  u64 shift = gl::MULT_GEN; int logn = C.lde_bits;
+  for (size_t s = 0; s < C.arities.size(); s++) {
+    int ab = C.arities[s], ar = 1 << ab;
+    const auto& v = layers.back();
+    size_t nl = v.size() / ar;
+    std::vector<Digest> leaves(nl);
+    std::vector<u64> flat(2 * ar);
+    for (size_t jj = 0; jj < nl; jj++) {
+      for (int k = 0; k < ar; k++) { flat[2 * k] = v[jj * ar + k].a; flat[2 * k + 1] = v[jj * ar + k].b; }
+      sponge(flat.data(), flat.size(), leaves[jj].e);
+    }
+    Tree t; t.build(std::move(leaves), logn - ab, C.cap_height);
+    d.absorb_digests(t.cap());
+    E beta = d.squeeze_e();
+    betas_fri.push_back(beta);
+    // fold: new[j] = interpolant through coset j at beta
+    u64 eta_b = gl::subgroup_gen(logn), om = gl::subgroup_gen(ab);
+    u64 om_inv = gl::inv(om), inv_ar = gl::inv((u64)ar);
+    std::vector<E> nv(nl);
+    std::vector<E> vals(ar);
+    for (size_t jj = 0; jj < nl; jj++) {
+      u64 ofs = gl::mul(shift, gl::pow(eta_b, gl::rev_bits(logn, (uint32_t)(jj << ab))));
+      for (int k = 0; k < ar; k++) vals[gl::rev_bits(ab, (uint32_t)k)] = v[jj * ar + k];
+      // coefficients of P(ofs*Y): c_k = (1/ar) sum_j vals_j om^{-jk}
+      std::vector<E> c(vals);
+      efft(c, ab, om_inv);
+      // P(beta) = sum_k c_k (beta/ofs)^k / ar
+      E bo = gl::escale(gl::inv(ofs), beta);
+      E acc = gl::e0();
+      for (int k = ar; k-- > 0;) acc = gl::eadd(gl::emul(acc, bo), c[k]);
+      nv[jj] = gl::escale(inv_ar, acc);
+    }
+    step_trees.push_back(std::move(t));
+    layers.push_back(std::move(nv));
+    shift = gl::pow(shift, (u64)ar);
+    logn -= ab;
+  }
+  // final polynomial: values on shift*<eta_f> (bit-reversed) -> coefficients
+  std::vector<E> fin = layers.back();
+  size_t nf = fin.size();
+  std::vector<E> nat(nf);
+  for (size_t i = 0; i < nf; i++) nat[gl::rev_bits(logn, (uint32_t)i)] = fin[i];
+  efft(nat, logn, gl::inv(gl::subgroup_gen(logn)));
+  u64 inv_nf = gl::inv((u64)nf), sinv = gl::inv(shift), sp = 1;
+  size_t final_len = (size_t)1 << (C.degree_bits - (int)C.arities.size() * C.arity_bits);
+  std::vector<E> final_poly(final_len);
+  for (size_t k = 0; k < nf; k++) {
+    E ck = gl::escale(gl::mul(inv_nf, sp), nat[k]);
+    sp = gl::mul(sp, sinv);
+    if (k < final_len) final_poly[k] = ck;
+    else if (!(ck.a == 0 && ck.b == 0)) throw std::runtime_error("generator: final polynomial has too high degree");
+  }
+  d.absorb_e(final_poly);
+  // proof of work: find w s.t. the top pow_bits of the squeezed response are zero
+  u64 mask = C.pow_bits ? (((1ULL << C.pow_bits) - 1) << (64 - C.pow_bits)) : 0;
+  u64 witness = 0;
+  for (u64 w = rg.next() & 0xFFFFFFFFULL;; w++) {
+    Duplex t = d; t.absorb(w);
+    u64 resp = t.squeeze();
+    if ((resp & mask) == 0) { witness = w; break; }
+  }
+  d.absorb(witness);
+  (void)d.squeeze();
+  std::vector<size_t> qidx(C.num_queries);
+  for (auto& q : qidx) q = (size_t)(d.squeeze() & (M - 1));
+
+  // ---------------------------------------------------------------- JSON
+  J j;
+  j.raw("{\"proof\":{\"wires_cap\":"); j.cap(W.wires_tree.cap());
+  j.raw(",\"plonk_zs_partial_products_cap\":"); j.cap(W.zs_tree.cap());
+  j.raw(",\"quotient_polys_cap\":"); j.cap(W.q_tree.cap());
+  j.raw(",\"openings\":{\"constants\":"); j.es(o_const); j.raw(",\"plonk_sigmas\":"); j.es(o_sig);
+  j.raw(",\"wires\":"); j.es(o_wires); j.raw(",\"plonk_zs\":"); j.es(o_zs); j.raw(",\"plonk_zs_next\":"); j.es(o_zs_next);
+  j.raw(",\"partial_products\":"); j.es(o_pp); j.raw(",\"quotient_polys\":"); j.es(o_quot);
+  j.raw(",\"lookup_zs\":"); j.es(o_lzs); j.raw(",\"lookup_zs_next\":"); j.es(o_lzs_next); j.raw("}");
+  j.raw(",\"opening_proof\":{\"commit_phase_merkle_caps\":[");
+  for (size_t s = 0; s < step_trees.size(); s++) { if (s) j.raw(","); j.cap(step_trees[s].cap()); }
+  j.raw("],\"query_round_proofs\":[");
+  for (int q = 0; q < C.num_queries; q++) {
+    if (q) j.raw(",");
+    size_t idx = qidx[q];
+    j.raw("{\"initial_trees_proof\":{\"evals_proofs\":[");
+    auto emit = [&](const u64* rowp, int width, const Tree& t, bool comma) {
+      if (comma) j.raw(",");
+      j.raw("["); j.fs(rowp, width); j.raw(",{\"siblings\":"); j.cap(t.path(idx)); j.raw("}]");
+    };
+    emit(&C.const_lde[idx * C.const_width], C.const_width, C.const_tree, false);
+    emit(&W.wires_lde[idx * C.num_wires], C.num_wires, W.wires_tree, true);
+    emit(&W.zs_lde[idx * W.zw], W.zw, W.zs_tree, true);
+    emit(&W.q_lde[idx * W.qw], W.qw, W.q_tree, true);
+    j.raw("]},\"steps\":[");
+    size_t qi = idx;
+    for (size_t s = 0; s < step_trees.size(); s++) {
+      int ab = C.arities[s], ar = 1 << ab;
+      size_t leaf = qi >> ab;
+      std::vector<E> ev(layers[s].begin() + leaf * ar, layers[s].begin() + (leaf + 1) * ar);
+      if (s) j.raw(",");
+      j.raw("{\"evals\":"); j.es(ev); j.raw(",\"merkle_proof\":{\"siblings\":"); j.cap(step_trees[s].path(leaf)); j.raw("}}");
+      qi = leaf;
+    }
+    j.raw("]}");
+  }
+  j.raw("],\"final_poly\":{\"coeffs\":"); j.es(final_poly); j.raw("},\"pow_witness\":"); j.u(witness); j.raw("}}");
+  j.raw(",\"public_inputs\":"); j.fs(pis.data(), pis.size()); j.raw("}");
+  return std::move(j.s);
+}
+
+thread_local std::string g_err;
+
+char* dupstr(const std::string& s) { char* p = (char*)malloc(s.size() + 1); memcpy(p, s.data(), s.size() + 1); return p; }
+
+}  // namespace
+
+extern "C" {
+
+// spec: degree_bits, num_public_inputs, lookups (0/1), circuit_seed
+void* p2v_gen_circuit_new(int degree_bits, int num_pis, int lookups, uint64_t circuit_seed, int num_queries, int pow_bits) {
+  try {
+    auto* C = new Circuit();
+    C->degree_bits = degree_bits; C->num_pis = num_pis; C->circuit_seed = circuit_seed;
+    if (num_queries > 0) C->num_queries = num_queries;
+    if (pow_bits >= 0) C->pow_bits = pow_bits;
+    if (lookups) {
+      C->nlp = 7;
+      std::vector<std::pair<u64, u64>> t8, t16;
+      for (u64 i = 0; i < 256; i++) t8.push_back({i, (i * i + 7) & 255});
+      int big = lookups > 1 ? 65536 : 1000;
+      for (u64 i = 0; i < (u64)big; i++) t16.push_back({i, 0});
+      C->luts.push_back(t8); C->luts.push_back(t16);
+    }
+    build_circuit(*C);
+    return C;
+  } catch (std::exception& e) { g_err = e.what(); return nullptr; }
+}
+void p2v_gen_circuit_free(void* c) { delete (Circuit*)c; }
+const char* p2v_gen_common_json(void* c) { return ((Circuit*)c)->common_json.c_str(); }
+const char* p2v_gen_vkey_json(void* c) { return ((Circuit*)c)->vkey_json.c_str(); }
+void* p2v_gen_witness_new(void* c, uint64_t seed) {
+  try { return make_witness(*(Circuit*)c, seed); } catch (std::exception& e) { g_err = e.what(); return nullptr; }
+}
+void p2v_gen_witness_free(void* w) { delete (Witness*)w; }
+char* p2v_gen_proof_json(void* c, void* w, uint64_t pi_seed) {
+  try { return dupstr(make_proof(*(Circuit*)c, *(Witness*)w, pi_seed)); } catch (std::exception& e) { g_err = e.what(); return nullptr; }
+}
+void p2v_gen_free_str(char* s) { free(s); }
+const char* p2v_gen_last_error(void) { return g_err.c_str(); }
+
+}  // extern "C"

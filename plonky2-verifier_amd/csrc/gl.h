@@ -1,0 +1,172 @@
+// gl.h — Goldilocks field p = 2^64 - 2^32 + 1 and its quadratic extension F[X]/(X^2-7),
+// shared by host C++ and the gfx950 device code.
+//
+// Semantics follow the reference (src/Algebra/Goldilocks.hs:126-175,
+// src/Algebra/GoldilocksExt.hs:54-100): every public operation returns the canonical
+// representative in [0, p); inv(0) = 0 (the reference computes inv as x^(p-2)).
+//
+// Device multiply: a 64x64 product is built from 32x32->64 partial products
+// (v_mad_u64_u32) and reduced with 2^64 = 2^32 - 1 (mod p), 2^96 = -1 (mod p).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define GL_HD __host__ __device__ __forceinline__
+#else
+#define GL_HD static inline
+#ifndef __host__
+#define __host__
+#define __device__
+#define __forceinline__ inline __attribute__((always_inline))
+#endif
+#endif
+
+namespace gl {
+
+static constexpr uint64_t P = 0xFFFFFFFF00000001ULL;
+static constexpr uint64_t EPS = 0xFFFFFFFFULL;           // 2^64 mod p
+static constexpr uint64_t MULT_GEN = 0xc65c18b67785d900ULL;      // Goldilocks.hs:51-52
+static constexpr uint64_t TWO_ADIC_GEN = 0x64fdd1a46201e246ULL;  // Goldilocks.hs:55-56
+
+GL_HD uint64_t canon(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return x >= P ? x - P : x;
+#else
+  uint64_t y; bool b = __builtin_sub_overflow(x, P, &y);
+  return b ? x : y;
+#endif
+}
+
+// (hi:lo) 128-bit value -> [0, 2^64) congruent mod p (not necessarily canonical)
+GL_HD uint64_t reduce128_nc(uint64_t hi, uint64_t lo) {
+  uint64_t hi_hi = hi >> 32;
+  uint64_t hi_lo = hi & EPS;
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t t0 = lo - hi_hi;
+  if (lo < hi_hi) t0 -= EPS;
+  uint64_t t1 = (hi_lo << 32) - hi_lo;
+  uint64_t r = t0 + t1;
+  if (r < t1) r += EPS;
+#else
+  uint64_t t0, r;
+  bool br = __builtin_sub_overflow(lo, hi_hi, &t0);
+  t0 -= EPS & (0 - (uint64_t)br);
+  uint64_t t1 = (hi_lo << 32) - hi_lo;
+  bool cy = __builtin_add_overflow(t0, t1, &r);
+  r += EPS & (0 - (uint64_t)cy);
+#endif
+  return r;
+}
+GL_HD uint64_t reduce128(uint64_t hi, uint64_t lo) { return canon(reduce128_nc(hi, lo)); }
+
+// hi < 2^32: value hi*2^64 + lo
+GL_HD uint64_t reduce96_nc(uint64_t hi, uint64_t lo) {
+  uint64_t t1 = (hi << 32) - hi;
+  uint64_t r = lo + t1;
+  if (r < t1) r += EPS;
+  return r;
+}
+
+GL_HD void mul128(uint64_t a, uint64_t b, uint64_t& hi, uint64_t& lo) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+  uint64_t p00 = (uint64_t)a0 * b0;
+  uint64_t p01 = (uint64_t)a0 * b1 + (p00 >> 32);          // < 2^64
+  uint64_t p10 = (uint64_t)a1 * b0 + (uint32_t)p01;        // < 2^64
+  lo = (p10 << 32) | (uint32_t)p00;
+  hi = (uint64_t)a1 * b1 + (p01 >> 32) + (p10 >> 32);
+#else
+  unsigned __int128 t = (unsigned __int128)a * b;
+  lo = (uint64_t)t; hi = (uint64_t)(t >> 64);
+#endif
+}
+
+GL_HD uint64_t add(uint64_t a, uint64_t b) {   // a, b canonical
+  uint64_t s = a + b;
+  uint64_t r = s + ((s < a) ? EPS : 0);          // wrapped: +2^64 == +EPS
+  return canon(r);
+}
+GL_HD uint64_t sub(uint64_t a, uint64_t b) {   // a, b canonical
+  uint64_t d = a - b;
+  return (a < b) ? d + P : d;
+}
+GL_HD uint64_t neg(uint64_t a) { return a ? P - a : 0; }
+GL_HD uint64_t mul(uint64_t a, uint64_t b) { uint64_t hi, lo; mul128(a, b, hi, lo); return reduce128(hi, lo); }
+GL_HD uint64_t sqr(uint64_t a) { return mul(a, a); }
+// multiply by a small constant c < 2^32
+GL_HD uint64_t mul_small(uint64_t a, uint32_t c) {
+  uint64_t lo = (uint64_t)(uint32_t)a * c;
+  uint64_t hi = (a >> 32) * (uint64_t)c;           // < 2^64
+  uint64_t l = lo + (hi << 32);
+  uint64_t h = (hi >> 32) + (l < lo ? 1 : 0);
+  return canon(reduce96_nc(h, l));
+}
+GL_HD uint64_t pow(uint64_t x, uint64_t e) {
+  uint64_t acc = 1, s = x;
+  while (e) { if (e & 1) acc = mul(acc, s); s = mul(s, s); e >>= 1; }
+  return acc;
+}
+GL_HD uint64_t inv(uint64_t x) { return pow(x, P - 2); }   // inv(0) = 0, as the reference
+
+// rootsOfUnity!k, Goldilocks.hs:68-74
+GL_HD uint64_t subgroup_gen(int k) {
+  uint64_t x = TWO_ADIC_GEN;
+  for (int i = 0; i < 32 - k; i++) x = mul(x, x);
+  return x;
+}
+
+GL_HD uint32_t rev_bits(int n, uint32_t w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return n ? (__brev(w) >> (32 - n)) : 0;
+#else
+  uint32_t r = 0;
+  for (int k = 0; k < n; k++) r |= ((w >> k) & 1u) << (n - k - 1);
+  return r;
+#endif
+}
+
+// ---------------------------------------------------------------- F^2 = F[X]/(X^2-7)
+struct E { uint64_t a, b; };
+GL_HD E e0() { return E{0, 0}; }
+GL_HD E eb(uint64_t x) { return E{x, 0}; }
+GL_HD E eadd(E x, E y) { return E{add(x.a, y.a), add(x.b, y.b)}; }
+GL_HD E esub(E x, E y) { return E{sub(x.a, y.a), sub(x.b, y.b)}; }
+GL_HD E eneg(E x) { return E{neg(x.a), neg(x.b)}; }
+GL_HD E escale(uint64_t s, E x) { return E{mul(s, x.a), mul(s, x.b)}; }
+GL_HD bool eeq(E x, E y) { return x.a == y.a && x.b == y.b; }
+GL_HD E emul(E x, E y) {
+  // (a + bX)(c + dX) = (ac + 7bd) + (ad + bc)X, lazily reduced: one reduction per limb
+  uint64_t h0, l0, h1, l1, h2, l2, h3, l3;
+  mul128(x.a, y.a, h0, l0);
+  mul128(x.b, y.b, h1, l1);
+  uint64_t bd = reduce128_nc(h1, l1);            // < 2^64
+  // ac + 7*bd as 128-bit
+  uint64_t s7l = (uint64_t)(uint32_t)bd * 7, s7h = (bd >> 32) * 7;
+  uint64_t t7 = s7l + (s7h << 32); uint64_t c7 = (s7h >> 32) + (t7 < s7l ? 1 : 0);
+  uint64_t ra = l0 + t7; uint64_t rh = h0 + c7 + (ra < l0 ? 1 : 0);
+  mul128(x.a, y.b, h2, l2);
+  mul128(x.b, y.a, h3, l3);
+  uint64_t rb = l2 + l3; uint64_t rbh = h2 + h3 + (rb < l2 ? 1 : 0);   // h2+h3 < 2^64 since hi < 2^64-1 each... see note
+  // note: h2,h3 <= 2^64-2 each; their sum may wrap.  Keep a third word.
+  uint64_t rbhh = (rbh < h2) ? 1 : 0;
+  if (rbhh) { // 2^128 = (2^64)^2 = EPS^2 mod p ; fold: add EPS^2 mod p = 0xfffffffe00000001 (2^64-2^33+1)
+    uint64_t f = 0xFFFFFFFE00000001ULL;
+    uint64_t r2 = rb + f; rbh += (r2 < rb ? 1 : 0); rb = r2;
+  }
+  return E{reduce128(rh, ra), reduce128(rbh, rb)};
+}
+GL_HD E esqr(E x) { return emul(x, x); }
+GL_HD E einv(E x) {   // invExt: conj / norm, norm = a^2 - 7b^2; 0 -> 0
+  uint64_t n = sub(mul(x.a, x.a), mul_small(mul(x.b, x.b), 7));
+  uint64_t d = inv(n);
+  return E{mul(x.a, d), mul(neg(x.b), d)};
+}
+GL_HD E ediv(E u, E v) { return emul(u, einv(v)); }
+GL_HD E epow(E x, uint64_t e) {
+  E acc = eb(1), s = x;
+  while (e) { if (e & 1) acc = emul(acc, s); s = emul(s, s); e >>= 1; }
+  return acc;
+}
+
+}  // namespace gl

@@ -1,0 +1,91 @@
+// poseidon.h — Plonky2 Poseidon-12 permutation over Goldilocks, host + gfx950 device.
+//
+// Restates src/Hash/Poseidon.hs:42-101 (4 full + 22 partial + 4 full rounds, x^7 S-box,
+// MDS = circulant(MDS_MATRIX_CIRC) + diag(MDS_MATRIX_DIAG), Hash/Constants.hs:19-25).
+// The device form keeps the 12-word state in VGPRs (one permutation per lane); round
+// constants are wave-uniform scalar loads from __constant__ memory; the MDS entries are
+// compile-time immediates (< 2^6) so each row is a 12-term small-constant dot product
+// accumulated in 64-bit halves and reduced once.
+#pragma once
+#include "gl.h"
+#include "poseidon_constants.h"
+
+namespace p2 {
+
+static constexpr uint32_t MDS_CIRC[12] = {17, 15, 41, 16, 2, 28, 13, 13, 39, 18, 34, 20};
+static constexpr uint32_t MDS_DIAG0 = 8;
+__host__ __device__ constexpr uint32_t mds_coeff(int i, int j) {
+  return MDS_CIRC[((j - i) % 12 + 12) % 12] + (i == j && i == 0 ? MDS_DIAG0 : 0);
+}
+
+#if defined(__HIPCC__)
+static __constant__ uint64_t c_round_constants[360] = P2V_ALL_ROUND_CONSTANTS_INIT;
+#endif
+static const uint64_t h_round_constants[360] = P2V_ALL_ROUND_CONSTANTS_INIT;
+
+// x^7
+__host__ __device__ __forceinline__ uint64_t sbox(uint64_t x) {
+  uint64_t x2 = gl::mul(x, x);
+  uint64_t x3 = gl::mul(x, x2);
+  uint64_t x4 = gl::mul(x2, x2);
+  return gl::mul(x3, x4);
+}
+
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__clang__)
+#define P2_UNROLL _Pragma("unroll")
+#else
+#define P2_UNROLL _Pragma("GCC unroll 12")
+#endif
+
+// y = M x with M = circ + diag; inputs canonical, outputs canonical.
+__host__ __device__ __forceinline__ void mds(uint64_t s[12]) {
+  uint64_t out[12];
+  P2_UNROLL
+  for (int i = 0; i < 12; i++) {
+    uint64_t al = 0, ah = 0;
+    P2_UNROLL
+    for (int j = 0; j < 12; j++) {
+      const uint64_t c = mds_coeff(i, j);
+      al += (uint64_t)(uint32_t)s[j] * c;
+      ah += (s[j] >> 32) * c;
+    }
+    // value = ah * 2^32 + al,  al, ah < 2^42
+    uint64_t l = al + (ah << 32);
+    uint64_t h = (ah >> 32) + (l < al ? 1 : 0);
+    out[i] = gl::canon(gl::reduce96_nc(h, l));
+  }
+  P2_UNROLL
+  for (int i = 0; i < 12; i++) s[i] = out[i];
+}
+
+__host__ __device__ __forceinline__ uint64_t round_constant(int idx) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return c_round_constants[idx];
+#else
+  return h_round_constants[idx];
+#endif
+}
+
+__host__ __device__ __forceinline__ void full_round(uint64_t s[12], int r) {
+  P2_UNROLL
+  for (int i = 0; i < 12; i++) s[i] = sbox(gl::add(s[i], round_constant(12 * r + i)));
+  mds(s);
+}
+__host__ __device__ __forceinline__ void partial_round(uint64_t s[12], int r) {
+  s[0] = sbox(gl::add(s[0], round_constant(12 * r)));
+  P2_UNROLL
+  for (int i = 1; i < 12; i++) s[i] = gl::add(s[i], round_constant(12 * r + i));
+  mds(s);
+}
+
+// Hash/Poseidon.hs:42-46
+__host__ __device__ __forceinline__ void permute(uint64_t s[12]) {
+#pragma unroll 1
+  for (int r = 0; r < 4; r++) full_round(s, r);
+#pragma unroll 1
+  for (int r = 4; r < 26; r++) partial_round(s, r);
+#pragma unroll 1
+  for (int r = 26; r < 30; r++) full_round(s, r);
+}
+
+}  // namespace p2
