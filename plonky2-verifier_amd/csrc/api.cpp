@@ -1,0 +1,304 @@
+// api.cpp — the C-ABI of libp2v (include/p2v.h): the drop-in boundary for
+// verifyProof :: VerifierCircuitData -> ProofWithPublicInputs -> Bool
+// (reference src/Plonk/Verifier.hs:56-65), batched, on MI355X.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+#include "../../include/p2v.h"
+#include "circuit.hpp"
+#include "dev.h"
+#include "gl.h"
+
+extern "C" __global__ void k_transpose(const uint64_t*, int64_t, int, uint64_t*, int);
+extern "C" __global__ void k_phase1(DevCircuit, int);
+extern "C" __global__ void k_merkle(DevCircuit);
+extern "C" __global__ void k_fri(DevCircuit);
+extern "C" __global__ void k_vanish(DevCircuit);
+extern "C" __global__ void k_status(DevCircuit, int8_t*, uint64_t*, int64_t);
+
+using namespace p2v;
+
+namespace {
+thread_local std::string g_err;
+int fail(int code, const std::string& msg) { g_err = msg; return code; }
+
+const char* kKernelNames = "k_transpose,k_phase1,k_merkle,k_fri,k_vanish,k_status";
+constexpr int kNumKernels = 6;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipError_t alloc(size_t n) { bytes = n; return hipMalloc(&p, n ? n : 16); }
+  void free_() { if (p) (void)hipFree(p); p = nullptr; }
+};
+}  // namespace
+
+struct p2v_circuit { Circuit c; };
+
+namespace {
+template <class T>
+hipError_t upload(DevBuf& b, const std::vector<T>& h) {
+  hipError_t e = b.alloc(h.size() * sizeof(T));
+  if (e != hipSuccess) return e;
+  if (!h.empty()) e = hipMemcpy(b.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
+  return e;
+}
+
+}  // namespace
+
+
+struct p2v_verifier {
+  const p2v_circuit* circ = nullptr;
+  int device = 0;
+  size_t max_batch = 0, Bmax = 0;
+  DevCircuit dc{};
+  std::vector<DevBuf> bufs;
+  DevBuf in, soa, chal, leafdig, mk, fbits, qvals, van, res, trace;
+  DevBuf t_cs, t_kis, t_gkind, t_gpar, t_ggrp, t_gwoff, t_w, t_gs, t_ge, t_lin, t_lout, t_loff, t_llen, t_tw, t_ops;
+  hipEvent_t ev[kNumKernels + 1];
+  float last_ms[kNumKernels] = {0};
+  bool timed = false;
+};
+
+extern "C" {
+
+const char* p2v_last_error_message(void) { return g_err.c_str(); }
+const char* p2v_version(void) { return "p2v 0.1.0 (gfx950)"; }
+const char* p2v_kernel_names(void) { return kKernelNames; }
+
+int p2v_circuit_from_json(const char* common_json, size_t common_len, const char* vkey_json, size_t vkey_len, p2v_circuit** out) {
+  if (!common_json || !vkey_json || !out) return fail(P2V_E_ARG, "null argument");
+  try {
+    JVal cj = parse_json(common_json, common_len);
+    JVal vj = parse_json(vkey_json, vkey_len);
+    auto* pc = new p2v_circuit();
+    pc->c = parse_circuit(cj, vj);
+    *out = pc;
+    return P2V_OK;
+  } catch (const ParseError& e) { return fail(P2V_E_PARSE, e.what()); }
+  catch (const CircuitError& e) { return fail(P2V_E_CIRCUIT, e.what()); }
+  catch (const std::exception& e) { return fail(P2V_E_PARSE, e.what()); }
+}
+
+void p2v_circuit_free(p2v_circuit* c) { delete c; }
+
+int p2v_circuit_get_info(const p2v_circuit* pc, p2v_circuit_info* info) {
+  if (!pc || !info) return fail(P2V_E_ARG, "null argument");
+  const Circuit& c = pc->c;
+  memset(info, 0, sizeof *info);
+  info->degree_bits = c.degree_bits; info->lde_bits = c.lde_bits; info->cap_height = c.cap_height;
+  info->num_challenges = c.r; info->num_query_rounds = c.num_queries; info->num_fri_steps = (int)c.arities.size();
+  info->final_poly_len = c.final_len; info->num_public_inputs = c.num_pis;
+  info->num_openings_this = (int)c.L.n_this; info->num_openings_next = (int)c.L.n_next;
+  info->has_lookups = c.lut_in.empty() ? 0 : 1; info->num_gates = (int)c.gates.size();
+  info->proof_words = c.L.words; info->trace_words = c.trace_words;
+  for (int t = 0; t < 4; t++) info->oracle_widths[t] = c.oracle_width[t];
+  for (size_t s = 0; s < c.arities.size() && s < 8; s++) info->step_arity_bits[s] = c.arities[s];
+  return P2V_OK;
+}
+
+int p2v_pack_proof_json(const p2v_circuit* pc, const char* proof_json, size_t len, uint64_t* dst) {
+  if (!pc || !proof_json || !dst) return fail(P2V_E_ARG, "null argument");
+  try {
+    JVal pj = parse_json(proof_json, len);
+    pack_proof(pc->c, pj, dst);
+    return P2V_OK;
+  } catch (const ShapeError& e) { return fail(P2V_E_SHAPE, e.what()); }
+  catch (const ParseError& e) { return fail(P2V_E_PARSE, e.what()); }
+  catch (const std::exception& e) { return fail(P2V_E_PARSE, e.what()); }
+}
+
+int p2v_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+#define HCK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { return fail(P2V_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); } } while (0)
+
+void p2v_verifier_free(p2v_verifier* v) {
+  if (!v) return;
+  (void)hipSetDevice(v->device);
+  for (DevBuf* b : {&v->in, &v->soa, &v->chal, &v->leafdig, &v->mk, &v->fbits, &v->qvals, &v->van, &v->res, &v->trace, &v->t_cs, &v->t_kis,
+                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops})
+    b->free_();
+  if (v->timed) for (auto& e : v->ev) (void)hipEventDestroy(e);
+  delete v;
+}
+
+int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v_verifier** out) {
+  if (!pc || !out || max_batch == 0) return fail(P2V_E_ARG, "null argument / zero batch");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(P2V_E_NODEVICE, "no HIP device available: libp2v verifies on MI355X only (no CPU fallback)");
+  if (device < 0 || device >= ndev) return fail(P2V_E_ARG, "bad device index");
+  HCK(hipSetDevice(device));
+  const Circuit& C = pc->c;
+  auto* v = new p2v_verifier();
+  v->circ = pc; v->device = device; v->max_batch = max_batch;
+  v->Bmax = (max_batch + 63) / 64 * 64;
+  DevCircuit& d = v->dc;
+  memset(&d, 0, sizeof d);
+  d.r = C.r; d.Q = C.num_queries; d.S = (int)C.arities.size(); d.T = 4 + d.S;
+  d.num_pis = C.num_pis; d.cap_len = C.cap_len; d.degree_bits = C.degree_bits; d.lde_bits = C.lde_bits; d.pow_bits = C.pow_bits;
+  d.num_wires = C.num_wires; d.num_routed = C.num_routed; d.num_constants = C.num_constants; d.ngc = C.num_gate_consts;
+  d.ngroups = (int)C.grp_start.size(); d.nls = C.nls; d.nlp = C.nlp; d.npp = C.npp; d.qdf = C.qdf; d.nluts = (int)C.lut_in.size();
+  d.depth0 = C.depth0; d.final_len = C.final_len;
+  for (int t = 0; t < 4; t++) d.width[t] = C.oracle_width[t];
+  d.n_gates = C.n_gate_eval; d.n_pp_terms = (int)C.n_pp_terms_per_round; d.n_lookup_terms = (int)C.n_lookup_terms_per_round;
+  d.alpha_base_gates = C.alpha_base_gates;
+  const Layout& L = C.L;
+  d.pis = L.pis; d.wcap = L.wcap; d.zcap = L.zcap; d.qcap = L.qcap; d.o_const = L.o_const; d.o_sig = L.o_sig; d.o_wires = L.o_wires;
+  d.o_zs = L.o_zs; d.o_pp = L.o_pp; d.o_quot = L.o_quot; d.o_lzs = L.o_lzs; d.o_zs_next = L.o_zs_next; d.o_lzs_next = L.o_lzs_next;
+  d.n_this = L.n_this; d.n_next = L.n_next; d.ccaps = L.ccaps; d.final_poly = L.final_poly; d.pow = L.pow; d.q0 = L.q0; d.qstride = L.qstride;
+  for (int t = 0; t < 4; t++) { d.leaf[t] = L.leaf[t]; d.path[t] = L.path[t]; }
+  for (int s = 0; s < d.S; s++) { d.step_evals[s] = L.step_evals[s]; d.step_path[s] = L.step_path[s]; d.arity[s] = C.arities[s]; d.step_depth[s] = C.step_depth[s]; }
+  d.words = L.words;
+  for (int i = 0; i < 4; i++) d.digest[i] = C.digest[i];
+  { uint64_t x = gl::TWO_ADIC_GEN; for (int m = 0; m <= 32; m++) { d.root_pow2[m] = x; x = gl::mul(x, x); } }
+  {
+    uint64_t shift = gl::MULT_GEN; int logn = C.lde_bits;
+    for (int s = 0; s <= d.S; s++) {
+      d.step_shift[s] = shift; d.step_shift_inv[s] = gl::inv(shift);
+      if (s < d.S) { d.step_logn[s] = logn; d.inv_arity[s] = gl::inv(1ULL << C.arities[s]); shift = gl::pow(shift, 1ULL << C.arities[s]); logn -= C.arities[s]; }
+    }
+  }
+  // circuit tables
+  std::vector<int32_t> gkind, ggrp, gwoff; std::vector<int64_t> gpar; std::vector<uint64_t> wts;
+  for (int g = 0; g < C.n_gate_eval; g++) {
+    const GateDesc& gd = C.gates[g];
+    gkind.push_back(gd.kind); ggrp.push_back(C.sel_idx[g]);
+    gpar.push_back(gd.p0); gpar.push_back(gd.p1); gpar.push_back(gd.p2);
+    gwoff.push_back((int32_t)wts.size()); wts.insert(wts.end(), gd.weights.begin(), gd.weights.end());
+  }
+  gwoff.push_back((int32_t)wts.size());
+  std::vector<uint64_t> lin, lout; std::vector<int64_t> loff, llen;
+  for (size_t t = 0; t < C.lut_in.size(); t++) { loff.push_back((int64_t)lin.size()); llen.push_back((int64_t)C.lut_in[t].size()); lin.insert(lin.end(), C.lut_in[t].begin(), C.lut_in[t].end()); lout.insert(lout.end(), C.lut_out[t].begin(), C.lut_out[t].end()); }
+  std::vector<uint64_t> tw(256 * (size_t)(d.S ? d.S : 1), 0);
+  for (int s = 0; s < d.S; s++) {
+    int ab = C.arities[s];
+    uint64_t om_inv = gl::inv(gl::subgroup_gen(ab)), x = 1;
+    for (int j = 0; j < (1 << ab) && j < 256; j++) { tw[256 * s + j] = x; x = gl::mul(x, om_inv); }
+  }
+  std::vector<int32_t> gs(C.grp_start.begin(), C.grp_start.end()), ge(C.grp_end.begin(), C.grp_end.end());
+  // transcript op program: proofChallenges (Challenge/Verifier.hs:58-103) + friChallenges (Challenge/FRI.hs:65-104)
+  std::vector<int32_t> ops;
+  auto op = [&](int t, int64_t a_, int64_t n_) { ops.push_back(t); ops.push_back((int32_t)a_); ops.push_back((int32_t)n_); };
+  {
+    const int r = d.r, C4 = 4 * C.cap_len;
+    op(TOP_ABSORB_DIGEST, 0, 4);
+    op(TOP_ABSORB_CHAL, CH_PI(d), 4);
+    op(TOP_ABSORB_SOA, L.wcap, C4);
+    op(TOP_SQUEEZE, CH_BETA(d), r);
+    op(TOP_SQUEEZE, CH_GAMMA(d), r);
+    if (C.nlp > 0) { op(TOP_COPY, CH_DELTA(d), 2 * r); op(TOP_SQUEEZE, CH_DELTA(d) + 2 * r, 2 * r); }
+    else op(TOP_ZERO, CH_DELTA(d), 4 * r);
+    op(TOP_ABSORB_SOA, L.zcap, C4);
+    op(TOP_SQUEEZE, CH_ALPHA(d), r);
+    op(TOP_ABSORB_SOA, L.qcap, C4);
+    op(TOP_SQUEEZE, CH_ZETA(d), 2);
+    op(TOP_ABSORB_SOA, L.o_const, 2 * (L.n_this + L.n_next));
+    op(TOP_SQUEEZE, CH_FRI_ALPHA(d), 2);
+    for (int s = 0; s < d.S; s++) { op(TOP_ABSORB_SOA, L.ccaps + (int64_t)s * C4, C4); op(TOP_SQUEEZE, CH_FRI_BETA(d) + 2 * s, 2); }
+    op(TOP_ABSORB_SOA, L.final_poly, 2 * C.final_len);
+    op(TOP_ABSORB_SOA, L.pow, 1);
+    op(TOP_SQUEEZE, CH_POW(d), 1);
+    op(TOP_SQUEEZE_IDX, CH_QIDX(d), d.Q);
+  }
+  d.ntops = (int)(ops.size() / 3);
+  hipError_t e = hipSuccess;
+#define UP(buf, vec) if (e == hipSuccess) e = upload(buf, vec)
+  UP(v->t_cs, C.cs_cap); UP(v->t_kis, C.k_is); UP(v->t_gkind, gkind); UP(v->t_gpar, gpar); UP(v->t_ggrp, ggrp); UP(v->t_gwoff, gwoff);
+  UP(v->t_w, wts); UP(v->t_gs, gs); UP(v->t_ge, ge); UP(v->t_lin, lin); UP(v->t_lout, lout); UP(v->t_loff, loff); UP(v->t_llen, llen); UP(v->t_tw, tw); UP(v->t_ops, ops);
+#undef UP
+  const size_t B = v->Bmax;
+  const size_t chw = (size_t)(4 + 7 * d.r + 4 + 2 * d.S + 1 + d.Q + 4);
+  if (e == hipSuccess) e = v->in.alloc((size_t)L.words * max_batch * 8);
+  if (e == hipSuccess) e = v->soa.alloc((size_t)L.words * B * 8);
+  if (e == hipSuccess) e = v->chal.alloc(chw * B * 8);
+  if (e == hipSuccess) e = v->leafdig.alloc((size_t)d.Q * d.T * 4 * B * 8);
+  if (e == hipSuccess) e = v->mk.alloc((size_t)d.Q * d.T * B);
+  if (e == hipSuccess) e = v->fbits.alloc((size_t)d.Q * B * 4);
+  if (e == hipSuccess) e = v->qvals.alloc((size_t)d.Q * 6 * B * 8);
+  if (e == hipSuccess) e = v->van.alloc((size_t)(1 + 4 * d.r) * B * 8);
+  if (e == hipSuccess) e = v->res.alloc(B);
+  if (e == hipSuccess) e = v->trace.alloc((size_t)C.trace_words * B * 8);
+  if (e == hipSuccess) { for (auto& x : v->ev) { e = hipEventCreate(&x); if (e != hipSuccess) break; } v->timed = e == hipSuccess; }
+  if (e != hipSuccess) { p2v_verifier_free(v); return fail(P2V_E_DEVICE, std::string("device allocation: ") + hipGetErrorString(e)); }
+  d.cs_cap = (const uint64_t*)v->t_cs.p; d.k_is = (const uint64_t*)v->t_kis.p; d.gate_kind = (const int32_t*)v->t_gkind.p;
+  d.gate_par = (const int64_t*)v->t_gpar.p; d.gate_grp = (const int32_t*)v->t_ggrp.p; d.gate_woff = (const int32_t*)v->t_gwoff.p;
+  d.weights = (const uint64_t*)v->t_w.p; d.grp_start = (const int32_t*)v->t_gs.p; d.grp_end = (const int32_t*)v->t_ge.p;
+  d.lut_in = (const uint64_t*)v->t_lin.p; d.lut_out = (const uint64_t*)v->t_lout.p; d.lut_off = (const int64_t*)v->t_loff.p; d.lut_len = (const int64_t*)v->t_llen.p;
+  d.twiddles = (const uint64_t*)v->t_tw.p; d.tops = (const int32_t*)v->t_ops.p;
+  d.soa = (const uint64_t*)v->soa.p; d.chal = (uint64_t*)v->chal.p; d.leafdig = (uint64_t*)v->leafdig.p; d.mk_ok = (uint8_t*)v->mk.p;
+  d.fri_bits = (uint32_t*)v->fbits.p; d.qvals = (uint64_t*)v->qvals.p; d.van = (uint64_t*)v->van.p;
+  *out = v;
+  return P2V_OK;
+}
+
+int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* results, uint64_t* trace, void* stream_, uint32_t flags) {
+  if (!v || (!proofs && n) || !results) return fail(P2V_E_ARG, "null argument");
+  if (n > v->max_batch) return fail(P2V_E_ARG, "batch larger than max_batch");
+  if (n == 0) return P2V_OK;
+  HCK(hipSetDevice(v->device));
+  hipStream_t st = (hipStream_t)stream_;
+  const Circuit& C = v->circ->c;
+  DevCircuit d = v->dc;
+  d.n = (int)n;
+  d.B = (int)((n + 63) / 64 * 64);
+  const int64_t words = C.L.words;
+  const uint64_t* src = proofs;
+  if (!(flags & P2V_FLAG_INPUT_DEVICE)) {
+    HCK(hipMemcpyAsync(v->in.p, proofs, (size_t)words * n * 8, hipMemcpyHostToDevice, st));
+    src = (const uint64_t*)v->in.p;
+  }
+  int8_t* dres = (flags & P2V_FLAG_RESULT_DEVICE) ? results : (int8_t*)v->res.p;
+  uint64_t* dtrace = nullptr;
+  if (trace) dtrace = (flags & P2V_FLAG_RESULT_DEVICE) ? trace : (uint64_t*)v->trace.p;
+  const int NPB = d.B / 64;
+  const bool tm = v->timed;
+  if (tm) HCK(hipEventRecord(v->ev[0], st));
+  k_transpose<<<dim3((unsigned)((words + 63) / 64), NPB), 256, 0, st>>>(src, words, (int)n, (uint64_t*)v->soa.p, d.B);
+  if (tm) HCK(hipEventRecord(v->ev[1], st));
+  const int nt_blocks = (d.B + 255) / 256;
+  const int leaf_units = d.Q * d.T * NPB;
+  k_phase1<<<nt_blocks + (leaf_units + 3) / 4, 256, 0, st>>>(d, nt_blocks);
+  if (tm) HCK(hipEventRecord(v->ev[2], st));
+  k_merkle<<<(leaf_units + 3) / 4, 256, 0, st>>>(d);
+  if (tm) HCK(hipEventRecord(v->ev[3], st));
+  k_fri<<<(d.Q * NPB + 3) / 4, 256, 0, st>>>(d);
+  if (tm) HCK(hipEventRecord(v->ev[4], st));
+  k_vanish<<<(d.B + 255) / 256, 256, 0, st>>>(d);
+  if (tm) HCK(hipEventRecord(v->ev[5], st));
+  k_status<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(d, dres, dtrace, C.trace_words);
+  if (tm) HCK(hipEventRecord(v->ev[6], st));
+  HCK(hipGetLastError());
+  if (!(flags & P2V_FLAG_RESULT_DEVICE)) {
+    HCK(hipMemcpyAsync(results, dres, n, hipMemcpyDeviceToHost, st));
+    if (trace) HCK(hipMemcpyAsync(trace, dtrace, (size_t)C.trace_words * n * 8, hipMemcpyDeviceToHost, st));
+  }
+  if (!(flags & P2V_FLAG_NO_SYNC) || !(flags & P2V_FLAG_RESULT_DEVICE)) {
+    HCK(hipStreamSynchronize(st));
+    if (tm) for (int k = 0; k < kNumKernels; k++) { float ms = 0; if (hipEventElapsedTime(&ms, v->ev[k], v->ev[k + 1]) == hipSuccess) v->last_ms[k] = ms; }
+  }
+  return P2V_OK;
+}
+
+int p2v_verifier_last_timings(const p2v_verifier* v, float* out, int max) {
+  if (!v || !out) return 0;
+  int k = 0;
+  for (; k < kNumKernels && k < max; k++) out[k] = v->last_ms[k];
+  return k;
+}
+
+int p2v_verify_batch(const p2v_circuit* c, const uint64_t* proofs, size_t n, int8_t* results, int device) {
+  p2v_verifier* v = nullptr;
+  int rc = p2v_verifier_create(c, device, n ? n : 1, &v);
+  if (rc != P2V_OK) return rc;
+  rc = p2v_verifier_run(v, proofs, n, results, nullptr, nullptr, 0);
+  p2v_verifier_free(v);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,364 @@
+// circuit.cpp — VerifierCircuitData decode/validation, packed layout, proof packing.
+#include "circuit.hpp"
+#include <algorithm>
+#include <cstring>
+
+namespace p2v {
+
+// ------------------------------------------------------------------ gate strings
+// A restatement of the Parsec grammar of Gate/Parser.hs:112-240.  Every alternative is
+// wrapped in `try` there, so each pattern is matched from the start of the string; the
+// `withEOF` ones must consume everything, the others ignore trailing text.
+namespace {
+struct Cur {
+  const char* p;
+  void spaces() { while (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r' || *p == '\f' || *p == '\v') p++; }
+  bool lit(const char* s) { size_t n = strlen(s); if (strncmp(p, s, n)) return false; p += n; return true; }
+  bool ch(char c) { if (*p != c) return false; p++; return true; }
+  bool integer(int64_t* iv, uint64_t* fv) {
+    if (*p < '0' || *p > '9') return false;
+    uint64_t w = 0; unsigned __int128 m = 0;
+    while (*p >= '0' && *p <= '9') { unsigned d = (unsigned)(*p - '0'); w = w * 10 + d; m = (m * 10 + d) % GL_P; p++; }
+    if (iv) *iv = (int64_t)w;
+    if (fv) *fv = (uint64_t)m;
+    return true;
+  }
+  bool comma() { if (!ch(',')) return false; spaces(); return true; }
+  bool kv_int(const char* key, int64_t* v) { return lit(key) && (spaces(), ch(':')) && (spaces(), integer(v, nullptr)) && (spaces(), true); }
+  bool list(std::vector<uint64_t>* out) {
+    if (!ch('[')) return false;
+    spaces();
+    int64_t iv; uint64_t fv;
+    if (integer(&iv, &fv)) {
+      if (out) out->push_back(fv);
+      while (*p == ',') {
+        comma();
+        if (!integer(&iv, &fv)) return false;
+        if (out) out->push_back(fv);
+      }
+    }
+    if (!ch(']')) return false;
+    spaces();
+    return true;
+  }
+  bool kv_list(const char* key, std::vector<uint64_t>* out) { return lit(key) && (spaces(), ch(':')) && (spaces(), list(out)) && (spaces(), true); }
+  bool open(const char* name) { return lit(name) && (spaces(), ch('{')) && (spaces(), true); }
+  bool close() { spaces(); if (!ch('}')) return false; spaces(); return true; }
+  bool eof() const { return *p == 0; }
+};
+const char* kPhantom = "_phantom: PhantomData<plonky2_field::goldilocks_field::GoldilocksField>";
+}  // namespace
+
+GateDesc parse_gate_string(const std::string& s) {
+  GateDesc g; g.text = s;
+  const char* str = s.c_str();
+  int64_t a, b, c;
+  { Cur u{str}; if (u.open("ArithmeticGate") && u.kv_int("num_ops", &a) && u.close() && u.eof()) { g.kind = G_ARITH; g.p0 = a; return g; } }
+  { Cur u{str}; if (u.open("ArithmeticExtensionGate") && u.kv_int("num_ops", &a) && u.close() && u.eof()) { g.kind = G_ARITH_EXT; g.p0 = a; return g; } }
+  { Cur u{str}; if (u.open("BaseSumGate") && u.kv_int("num_limbs", &a) && u.close() && u.ch('+')) { u.spaces(); if (u.kv_int("Base", &b) && u.eof()) { g.kind = G_BASESUM; g.p0 = a; g.p1 = b; return g; } } }
+  { Cur u{str}; std::vector<uint64_t> w;
+    if (u.open("CosetInterpolationGate") && u.kv_int("subgroup_bits", &a) && u.comma() && u.kv_int("degree", &b) && u.comma() &&
+        u.kv_list("barycentric_weights", &w) && u.comma() && u.lit(kPhantom)) {
+      u.spaces();
+      if (u.close() && u.lit("<D=2>") && u.eof()) { g.kind = G_COSET; g.p0 = a; g.p1 = b; g.weights = w; return g; }
+    } }
+  { Cur u{str}; if (u.open("ConstantGate") && u.kv_int("num_consts", &a) && u.close()) { g.kind = G_CONST; g.p0 = a; return g; } }
+  { Cur u{str}; if (u.open("ExponentiationGate") && u.kv_int("num_power_bits", &a) && u.close()) { g.kind = G_EXP; g.p0 = a; return g; } }
+  { Cur u{str}; if (u.open("LookupGate") && u.kv_int("num_slots", &a) && u.comma() && u.kv_list("lut_hash", nullptr) && u.close()) { g.kind = G_LOOKUP; g.p0 = a; return g; } }
+  { Cur u{str}; if (u.open("LookupTableGate") && u.kv_int("num_slots", &a) && u.comma() && u.kv_list("lut_hash", nullptr) && u.comma() &&
+                    u.kv_int("last_lut_row", &c) && u.close()) { g.kind = G_LOOKUPTABLE; g.p0 = a; g.p2 = c; return g; } }
+  { Cur u{str}; if (u.open("MulExtensionGate") && u.kv_int("num_ops", &a) && u.close()) { g.kind = G_MULEXT; g.p0 = a; return g; } }
+  { Cur u{str}; if (u.lit("NoopGate")) { g.kind = G_NOOP; return g; } }
+  { Cur u{str}; if (u.lit("PublicInputGate")) { g.kind = G_PI; return g; } }
+  { Cur u{str}; if (u.lit("PoseidonGate(PhantomData<plonky2_field::goldilocks_field::GoldilocksField>)<WIDTH=") && u.integer(&a, nullptr) && u.ch('>') && u.eof()) { g.kind = G_POSEIDON; g.p0 = a; return g; } }
+  { Cur u{str}; if (u.lit("PoseidonMdsGate(PhantomData<plonky2_field::goldilocks_field::GoldilocksField>)<WIDTH=") && u.integer(&a, nullptr) && u.ch('>') && u.eof()) { g.kind = G_POSEIDON_MDS; g.p0 = a; return g; } }
+  { Cur u{str}; if (u.open("RandomAccessGate") && u.kv_int("bits", &a) && u.comma() && u.kv_int("num_copies", &b) && u.comma() &&
+                    u.kv_int("num_extra_constants", &c) && u.comma() && u.lit(kPhantom)) {
+      u.spaces();
+      if (u.close() && u.lit("<D=2>")) { g.kind = G_RANDACC; g.p0 = a; g.p1 = b; g.p2 = c; return g; }
+    } }
+  { Cur u{str}; if (u.open("ReducingGate") && u.kv_int("num_coeffs", &a)) { u.lit("<D=2>"); if (u.close()) { g.kind = G_REDUCING; g.p0 = a; return g; } } }
+  { Cur u{str}; if (u.open("ReducingExtensionGate") && u.kv_int("num_coeffs", &a)) { u.lit("<D=2>"); if (u.close()) { g.kind = G_REDUCING_EXT; g.p0 = a; return g; } } }
+  g.kind = G_UNKNOWN;
+  return g;
+}
+
+// highest wire / constant index a gate program reads (Gate/Constraints.hs, Gate/Custom/*):
+// the reference raises an Array index `error` when it exceeds the opening vectors.
+static void gate_footprint(const GateDesc& g, int64_t& max_wire, int64_t& max_const) {
+  max_wire = -1; max_const = -1;
+  switch (g.kind) {
+    case G_ARITH: if (g.p0 > 0) { max_wire = 4 * g.p0 - 1; max_const = 1; } break;
+    case G_ARITH_EXT: if (g.p0 > 0) { max_wire = 8 * g.p0 - 1; max_const = 1; } break;
+    case G_BASESUM: max_wire = std::max<int64_t>(g.p0, 1); break;
+    case G_COSET: {
+      int64_t n = (int64_t)1 << g.p0, d = g.p1;
+      int64_t nint = d - 1 != 0 ? (n - 2) / (d - 1) : 0;
+      max_wire = 1 + 2 * (n + 2) + 4 * nint + 1;
+      break; }
+    case G_CONST: if (g.p0 > 0) { max_wire = g.p0 - 1; max_const = g.p0 - 1; } break;
+    case G_EXP: max_wire = 2 * g.p0 + 1; break;
+    case G_MULEXT: if (g.p0 > 0) { max_wire = 6 * g.p0 - 1; max_const = 0; } break;
+    case G_PI: max_wire = 3; break;
+    case G_POSEIDON: max_wire = 29 + 36 + 22 + 48 - 1; break;
+    case G_POSEIDON_MDS: max_wire = 2 * 23 + 1; break;
+    case G_RANDACC: {
+      int64_t width = 2 + ((int64_t)1 << g.p0);
+      int64_t bstart = width * g.p1 + g.p2;
+      max_wire = std::max<int64_t>(bstart + g.p1 * g.p0 - 1, g.p1 * width + g.p2 - 1);
+      if (g.p2 > 0) max_const = g.p2 - 1;
+      break; }
+    case G_REDUCING: { int64_t n = g.p0; max_wire = std::max<int64_t>({5, n + 5, n >= 2 ? 3 * n + 3 : 5}); break; }
+    case G_REDUCING_EXT: { int64_t n = g.p0; max_wire = std::max<int64_t>({5, 2 * n + 5, n >= 2 ? 4 * n + 3 : 5}); break; }
+    default: break;
+  }
+}
+
+static void digest_of(const JVal& d, uint64_t* out) {   // Hash/Digest.hs:40-44
+  const auto& e = d.at("elements").arr();
+  if (e.size() != 4) throw ParseError("digest must have 4 elements");
+  for (int i = 0; i < 4; i++) out[i] = j_field(e[i]);
+}
+
+Circuit parse_circuit(const JVal& common, const JVal& vkey) {
+  Circuit C;
+  const JVal& cfg = common.at("config");
+  C.num_wires = (int)j_int(cfg.at("num_wires"));
+  C.num_routed = (int)j_int(cfg.at("num_routed_wires"));
+  C.num_gate_consts = (int)j_int(cfg.at("num_constants"));
+  (void)j_bool(cfg.at("use_base_arithmetic_gate"));
+  (void)j_int(cfg.at("security_bits"));
+  C.r = (int)j_int(cfg.at("num_challenges"));
+  (void)j_bool(cfg.at("zero_knowledge"));
+  (void)j_bool(cfg.at("randomize_unused_wires"));
+  C.max_qdf = (int)j_int(cfg.at("max_quotient_degree_factor"));
+  const JVal& fc = cfg.at("fri_config");
+  C.rate_bits = (int)j_int(fc.at("rate_bits"));
+  C.cap_height = (int)j_int(fc.at("cap_height"));
+  C.pow_bits = (int)j_int(fc.at("proof_of_work_bits"));
+  C.num_queries = (int)j_int(fc.at("num_query_rounds"));
+  const JVal& rs = fc.at("reduction_strategy");
+  if (rs.kind != JVal::Obj || rs.keys.size() != 1) throw ParseError("reduction_strategy: expecting a singleton object");
+  const JVal& fp = common.at("fri_params");
+  (void)j_bool(fp.at("hiding"));
+  C.degree_bits = (int)j_int(fp.at("degree_bits"));
+  (void)fp.at("reduction_arity_bits").arr();
+  (void)fp.at("config");
+  C.lde_bits = C.degree_bits + C.rate_bits;
+  // expandReductionStrategy starts from degree_bits (Plonk/FRI.hs:337-354, :378)
+  if (rs.keys[0] == "ConstantArityBits") {
+    const auto& ab = rs.items[0].arr();
+    if (ab.size() != 2) throw ParseError("ConstantArityBits: expecting [arity_bits, final_poly_bits]");
+    int a = (int)j_int(ab[0]), f = (int)j_int(ab[1]);
+    if (a <= 0 && C.degree_bits > f) throw CircuitError("reduction strategy does not terminate (arity_bits <= 0)");
+    for (int logn = C.degree_bits; logn > f; logn -= a) C.arities.push_back(a);
+  } else if (rs.keys[0] == "Fixed") {
+    for (const auto& x : rs.items[0].arr()) C.arities.push_back((int)j_int(x));
+  } else if (rs.keys[0] == "MinSize") {
+    throw CircuitError("reduction strategy not implemented (MinSize), Plonk/FRI.hs:342");
+  } else {
+    throw ParseError("FromJSON/FriReductionStrategy: unrecognized FRI reduction strategy");
+  }
+  for (const auto& g : common.at("gates").arr()) {
+    if (g.kind != JVal::Str) throw ParseError("gate must be a string");
+    C.gates.push_back(parse_gate_string(g.text));
+  }
+  const JVal& si = common.at("selectors_info");
+  for (const auto& x : si.at("selector_indices").arr()) C.sel_idx.push_back((int)j_int(x));
+  for (const auto& g : si.at("groups").arr()) { C.grp_start.push_back((int)j_int(g.at("start"))); C.grp_end.push_back((int)j_int(g.at("end"))); }
+  C.qdf = (int)j_int(common.at("quotient_degree_factor"));
+  C.num_gate_constraints = (int)j_int(common.at("num_gate_constraints"));
+  C.num_constants = (int)j_int(common.at("num_constants"));
+  C.num_pis = (int)j_int(common.at("num_public_inputs"));
+  for (const auto& x : common.at("k_is").arr()) C.k_is.push_back(j_field(x));
+  C.npp = (int)j_int(common.at("num_partial_products"));
+  C.nlp = (int)j_int(common.at("num_lookup_polys"));
+  C.nls = (int)j_int(common.at("num_lookup_selectors"));
+  for (const auto& t : common.at("luts").arr()) {
+    std::vector<uint64_t> in, out;
+    for (const auto& e : t.arr()) {
+      const auto& pr = e.arr();
+      if (pr.size() != 2) throw ParseError("lut entry must be a pair");
+      in.push_back(j_word64_mod_p(pr[0])); out.push_back(j_word64_mod_p(pr[1]));
+    }
+    C.lut_in.push_back(std::move(in)); C.lut_out.push_back(std::move(out));
+  }
+  for (const auto& d : vkey.at("constants_sigmas_cap").arr()) { uint64_t e[4]; digest_of(d, e); C.cs_cap.insert(C.cs_cap.end(), e, e + 4); }
+  digest_of(vkey.at("circuit_digest"), C.digest);
+
+  // ---------------------------------------------------------------- validation
+  // Circuit-level `error`s that the reference raises on every verification of this circuit.
+  const int ngroups = (int)C.grp_start.size();
+  const int nluts = (int)C.lut_in.size();
+  if (C.r <= 0 || C.r > 4) throw CircuitError("num_challenges must be in 1..4 (this build)");
+  if (C.cap_height < 0 || C.cap_height > 20 || C.degree_bits <= 0 || C.lde_bits > 30) throw CircuitError("unsupported FRI sizes");
+  if (C.nls != (nluts == 0 ? 0 : 4 + nluts)) throw CircuitError("getSelectorConfig: fatal: num_lookup_selectors /= (4 + #nluts)");
+  if (C.num_constants != ngroups + C.nls + C.num_gate_consts) throw CircuitError("getSelectorConfig: fatal: constant columns tally does not add up!");
+  C.n_gate_eval = (int)std::min(C.sel_idx.size(), C.gates.size());
+  if (C.n_gate_eval == 0) throw CircuitError("foldl1: empty gate list");
+  for (int g = 0; g < C.n_gate_eval; g++) {
+    const GateDesc& gd = C.gates[g];
+    if (gd.kind == G_UNKNOWN) throw CircuitError("gateConstraints: unknown gate `" + gd.text + "`");
+    if ((gd.kind == G_POSEIDON || gd.kind == G_POSEIDON_MDS) && gd.p0 != 12) throw CircuitError("PoseidonGate: unsupported width");
+    if (gd.kind == G_COSET && (gd.p1 < 2 || gd.p0 < 1 || gd.p0 > 10)) throw CircuitError("CosetInterpolationGate: unsupported parameters");
+    if (gd.kind == G_RANDACC && (gd.p0 < 0 || gd.p0 > 16)) throw CircuitError("RandomAccessGate: unsupported bits");
+    if (gd.kind == G_BASESUM && (gd.p1 < 0 || gd.p1 > (1 << 16))) throw CircuitError("BaseSumGate: unsupported base");
+    int grp = C.sel_idx[g];
+    if (grp < 0 || grp >= ngroups) throw CircuitError("selector_groups !! group_idx: index out of range");
+    int64_t mw, mc;
+    gate_footprint(gd, mw, mc);
+    if (mw >= C.num_wires) throw CircuitError("(Array.!): gate reads a wire beyond num_wires: " + gd.text);
+    if (mc >= C.num_gate_consts) throw CircuitError("(Array.!): gate reads a constant beyond num_constants: " + gd.text);
+  }
+  if (C.qdf <= 0) throw CircuitError("quotient_degree_factor must be positive");
+  if (C.npp <= 0) throw CircuitError("num_partial_products must be positive");
+  {
+    int npp_all = (C.num_routed + C.qdf - 1) / C.qdf;   // combineInitial sanity, Plonk/FRI.hs:168
+    if (C.r * (npp_all + C.nlp) != C.r * (1 + C.npp + C.nlp)) throw CircuitError("combineInitial: sanity check failed");
+  }
+  if ((int64_t)C.k_is.size() < C.num_routed) throw CircuitError("k_is shorter than num_routed_wires");
+  if (nluts > 0 && (C.nlp < 2 || C.num_routed < 3 || C.qdf < 2)) throw CircuitError("lookup argument: unsupported sizes");
+
+  // ---------------------------------------------------------------- derived shapes
+  C.cap_len = 1 << C.cap_height;
+  if ((int)C.cs_cap.size() != 4 * C.cap_len) throw CircuitError("validateMerkleCapLength: constants_sigmas_cap has wrong size");
+  int sum_a = 0; for (int a : C.arities) { if (a <= 0 || a > 8) throw CircuitError("unsupported FRI arity"); sum_a += a; }
+  if (sum_a > C.degree_bits) throw CircuitError("reduction strategy folds below degree 1");
+  if (C.arities.size() > 8) throw CircuitError("more than 8 FRI steps");
+  C.final_len = 1 << (C.degree_bits - sum_a);
+  C.oracle_width[0] = C.num_constants + C.num_routed;
+  C.oracle_width[1] = C.num_wires;
+  C.oracle_width[2] = C.r * (1 + C.npp + C.nlp);
+  C.oracle_width[3] = C.r * C.qdf;
+  C.depth0 = C.lde_bits - C.cap_height;
+  if (C.depth0 < 0) throw CircuitError("cap_height exceeds the LDE size");
+  { int logn = C.lde_bits; for (int a : C.arities) { logn -= a; C.step_depth.push_back(std::max(0, logn - C.cap_height)); } }
+  // term counts before the gate terms (Vanishing.hs:67-111, Lookups.hs:73-132)
+  {
+    int nnum = std::min<int>(C.num_routed, C.num_wires), nden = std::min<int>(C.num_routed, C.num_wires);
+    int nnc = (nnum + C.qdf - 1) / C.qdf, ndc = (nden + C.qdf - 1) / C.qdf;
+    int ncur = C.npp + 2;
+    C.n_pp_terms_per_round = std::min({ncur - 1, nnc, ndc});
+    C.n_lookup_terms_per_round = 0;
+    if (nluts > 0) {
+      int nlu = std::min(C.num_routed / 2, C.num_wires / 2), nlut = std::min(C.num_routed / 3, C.num_wires / 3);
+      int nsldc = C.nlp - 1, lu_degree = C.qdf - 1, lut_degree = (C.num_routed / 3 + nsldc - 1) / nsldc;
+      int nclu = (nlu + lu_degree - 1) / lu_degree, nclut = (nlut + lut_degree - 1) / lut_degree, ncm = (C.num_routed / 3 + lut_degree - 1) / lut_degree;
+      int nz = std::min({nclu, nclut, ncm, nsldc});
+      C.n_lookup_terms_per_round = 3 + nluts + 1 + 2 * nz;
+      if (3 * (C.num_routed / 3 - 1) + 2 >= C.num_wires) throw CircuitError("lookup mults beyond num_wires");
+    }
+    C.alpha_base_gates = C.r + C.r * C.n_pp_terms_per_round + (nluts > 0 ? C.r * C.n_lookup_terms_per_round : 0);
+  }
+  // ---------------------------------------------------------------- layout
+  Layout& L = C.L;
+  int64_t w = 0;
+  L.pis = w; w += C.num_pis;
+  L.wcap = w; w += 4 * C.cap_len;
+  L.zcap = w; w += 4 * C.cap_len;
+  L.qcap = w; w += 4 * C.cap_len;
+  L.open = w;
+  L.o_const = w; w += 2 * C.num_constants;
+  L.o_sig = w; w += 2 * C.num_routed;
+  L.o_wires = w; w += 2 * C.num_wires;
+  L.o_zs = w; w += 2 * C.r;
+  L.o_pp = w; w += 2 * C.r * C.npp;
+  L.o_quot = w; w += 2 * C.r * C.qdf;
+  L.o_lzs = w; w += 2 * C.r * C.nlp;
+  L.n_this = (w - L.open) / 2;
+  L.o_zs_next = w; w += 2 * C.r;
+  L.o_lzs_next = w; w += 2 * C.r * C.nlp;
+  L.n_next = (w - L.o_zs_next) / 2;
+  L.ccaps = w; w += (int64_t)C.arities.size() * 4 * C.cap_len;
+  L.final_poly = w; w += 2 * C.final_len;
+  L.pow = w; w += 1;
+  L.q0 = w;
+  int64_t q = 0;
+  for (int t = 0; t < 4; t++) { L.leaf[t] = q; q += C.oracle_width[t]; }
+  for (int t = 0; t < 4; t++) { L.path[t] = q; q += 4 * C.depth0; }
+  for (size_t s = 0; s < C.arities.size(); s++) {
+    L.step_evals.push_back(q); q += 2 * (1 << C.arities[s]);
+    L.step_path.push_back(q); q += 4 * C.step_depth[s];
+  }
+  L.qstride = q;
+  w += q * C.num_queries;
+  L.words = w;
+  const int S = (int)C.arities.size(), Q = C.num_queries, r = C.r;
+  C.trace_words = 4 + 3 * r + 4 * r + 4 + 2 * S + 1 + Q + 4 * r + 6 * Q + 1;
+  return C;
+}
+
+// ------------------------------------------------------------------ packing
+namespace {
+struct Packer {
+  const Circuit& C;
+  uint64_t* dst;
+  void fields(const JVal& v, int64_t off, int64_t n, const char* what) {
+    const auto& a = v.arr();
+    if ((int64_t)a.size() != n) throw ShapeError(std::string(what) + ": expected " + std::to_string(n) + " elements, got " + std::to_string(a.size()));
+    for (int64_t i = 0; i < n; i++) dst[off + i] = j_field(a[i]);
+  }
+  void exts(const JVal& v, int64_t off, int64_t n, const char* what) {
+    const auto& a = v.arr();
+    if ((int64_t)a.size() != n) throw ShapeError(std::string(what) + ": expected " + std::to_string(n) + " F^2 values, got " + std::to_string(a.size()));
+    for (int64_t i = 0; i < n; i++) {
+      const auto& pr = a[i].arr();
+      if (pr.size() != 2) throw ParseError("F^2 value must be a pair");
+      dst[off + 2 * i] = j_field(pr[0]); dst[off + 2 * i + 1] = j_field(pr[1]);
+    }
+  }
+  void digests(const JVal& v, int64_t off, int64_t n, const char* what) {
+    const auto& a = v.arr();
+    if ((int64_t)a.size() != n) throw ShapeError(std::string(what) + ": expected " + std::to_string(n) + " digests, got " + std::to_string(a.size()));
+    for (int64_t i = 0; i < n; i++) digest_of(a[i], dst + off + 4 * i);
+  }
+};
+}  // namespace
+
+void pack_proof(const Circuit& C, const JVal& root, uint64_t* dst) {
+  const Layout& L = C.L;
+  Packer P{C, dst};
+  const JVal& pr = root.at("proof");
+  P.fields(root.at("public_inputs"), L.pis, C.num_pis, "public_inputs");
+  P.digests(pr.at("wires_cap"), L.wcap, C.cap_len, "wires_cap");
+  P.digests(pr.at("plonk_zs_partial_products_cap"), L.zcap, C.cap_len, "plonk_zs_partial_products_cap");
+  P.digests(pr.at("quotient_polys_cap"), L.qcap, C.cap_len, "quotient_polys_cap");
+  const JVal& o = pr.at("openings");
+  P.exts(o.at("constants"), L.o_const, C.num_constants, "openings.constants");
+  P.exts(o.at("plonk_sigmas"), L.o_sig, C.num_routed, "openings.plonk_sigmas");
+  P.exts(o.at("wires"), L.o_wires, C.num_wires, "openings.wires");
+  P.exts(o.at("plonk_zs"), L.o_zs, C.r, "openings.plonk_zs");
+  P.exts(o.at("partial_products"), L.o_pp, (int64_t)C.r * C.npp, "openings.partial_products");
+  P.exts(o.at("quotient_polys"), L.o_quot, (int64_t)C.r * C.qdf, "openings.quotient_polys");
+  P.exts(o.at("lookup_zs"), L.o_lzs, (int64_t)C.r * C.nlp, "openings.lookup_zs");
+  P.exts(o.at("plonk_zs_next"), L.o_zs_next, C.r, "openings.plonk_zs_next");
+  P.exts(o.at("lookup_zs_next"), L.o_lzs_next, (int64_t)C.r * C.nlp, "openings.lookup_zs_next");
+  const JVal& fp = pr.at("opening_proof");
+  const auto& cc = fp.at("commit_phase_merkle_caps").arr();
+  const int S = (int)C.arities.size();
+  if ((int)cc.size() != S) throw ShapeError("commit_phase_merkle_caps: expected " + std::to_string(S));
+  for (int s = 0; s < S; s++) P.digests(cc[s], L.ccaps + (int64_t)s * 4 * C.cap_len, C.cap_len, "commit_phase_merkle_caps[s]");
+  P.exts(fp.at("final_poly").at("coeffs"), L.final_poly, C.final_len, "final_poly.coeffs");
+  dst[L.pow] = j_field(fp.at("pow_witness"));
+  const auto& qr = fp.at("query_round_proofs").arr();
+  if ((int)qr.size() != C.num_queries) throw ShapeError("query_round_proofs: expected " + std::to_string(C.num_queries));
+  for (int q = 0; q < C.num_queries; q++) {
+    int64_t base = L.q0 + (int64_t)q * L.qstride;
+    const auto& ep = qr[q].at("initial_trees_proof").at("evals_proofs").arr();
+    if (ep.size() != 4) throw ShapeError("checkInitialTreeProofs: expecting 4 Merkle proofs for the 4 oracles");
+    for (int t = 0; t < 4; t++) {
+      const auto& pair = ep[t].arr();
+      if (pair.size() != 2) throw ParseError("evals_proofs entry must be a pair");
+      P.fields(pair[0], base + L.leaf[t], C.oracle_width[t], "initial tree leaf");
+      P.digests(pair[1].at("siblings"), base + L.path[t], C.depth0, "initial tree siblings");
+    }
+    const auto& st = qr[q].at("steps").arr();
+    if ((int)st.size() != S) throw ShapeError("steps: expected " + std::to_string(S));
+    for (int s = 0; s < S; s++) {
+      P.exts(st[s].at("evals"), base + L.step_evals[s], 1 << C.arities[s], "step evals");
+      P.digests(st[s].at("merkle_proof").at("siblings"), base + L.step_path[s], C.step_depth[s], "step siblings");
+    }
+  }
+}
+
+}  // namespace p2v

@@ -1,0 +1,74 @@
+// circuit.hpp — host side of the drop-in boundary: decode VerifierCircuitData
+// (reference src/Types.hs:47-240, Gate strings src/Gate/Parser.hs:27-242), validate it
+// once (circuit-level `error`s of the reference surface here), derive the fixed packed
+// proof layout, and pack ProofWithPublicInputs JSON (Types.hs:245-279) into it.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+#include "json.hpp"
+
+namespace p2v {
+
+enum GateKind : int32_t {   // Gate/Base.hs:27-45
+  G_ARITH = 0, G_ARITH_EXT, G_BASESUM, G_COSET, G_CONST, G_EXP, G_LOOKUP, G_LOOKUPTABLE,
+  G_MULEXT, G_NOOP, G_PI, G_POSEIDON, G_POSEIDON_MDS, G_RANDACC, G_REDUCING, G_REDUCING_EXT, G_UNKNOWN
+};
+
+struct GateDesc {
+  int32_t kind = G_UNKNOWN;
+  int64_t p0 = 0, p1 = 0, p2 = 0;
+  std::vector<uint64_t> weights;   // CosetInterpolationGate barycentric weights
+  std::string text;
+};
+
+// Fixed per-circuit packed proof layout (u64 words).  Order:
+//   pis | wires_cap | zs_pp_cap | quotient_cap | openings(batch_this ++ batch_next)
+//   | commit caps | final poly | pow witness | Q x [4 leaves | 4 paths | steps x (evals | path)]
+struct Layout {
+  int64_t pis = 0, wcap = 0, zcap = 0, qcap = 0;
+  int64_t open = 0;                         // start of the F^2 openings (2 words each)
+  int64_t o_const = 0, o_sig = 0, o_wires = 0, o_zs = 0, o_pp = 0, o_quot = 0, o_lzs = 0;   // batch_this
+  int64_t o_zs_next = 0, o_lzs_next = 0;    // batch_next
+  int64_t n_this = 0, n_next = 0;           // F^2 counts
+  int64_t ccaps = 0, final_poly = 0, pow = 0;
+  int64_t q0 = 0, qstride = 0;
+  int64_t leaf[4] = {0, 0, 0, 0}, path[4] = {0, 0, 0, 0};   // offsets inside one query
+  std::vector<int64_t> step_evals, step_path;                 // offsets inside one query
+  int64_t words = 0;
+};
+
+struct Circuit {
+  // CircuitConfig (Types.hs:73-84)
+  int num_wires = 0, num_routed = 0, num_gate_consts = 0, r = 0, max_qdf = 0;
+  // FriConfig / FriParams (Types.hs:116-174)
+  int rate_bits = 0, cap_height = 0, pow_bits = 0, num_queries = 0, degree_bits = 0, lde_bits = 0;
+  std::vector<int> arities;                 // expandReductionStrategy, Plonk/FRI.hs:337-354
+  // CommonCircuitData (Types.hs:47-61)
+  std::vector<GateDesc> gates;
+  std::vector<int> sel_idx;
+  std::vector<int> grp_start, grp_end;
+  int qdf = 0, num_gate_constraints = 0, num_constants = 0, num_pis = 0;
+  std::vector<uint64_t> k_is;
+  int npp = 0, nlp = 0, nls = 0;
+  std::vector<std::vector<uint64_t>> lut_in, lut_out;
+  // VerifierOnlyCircuitData (Types.hs:236-240)
+  std::vector<uint64_t> cs_cap;             // 4 words per digest
+  uint64_t digest[4] = {0, 0, 0, 0};
+  // derived
+  int cap_len = 0, final_len = 0;
+  int oracle_width[4] = {0, 0, 0, 0};
+  int depth0 = 0;                           // initial Merkle path length
+  std::vector<int> step_depth;
+  int n_gate_eval = 0;                      // gates actually evaluated: min(#selector_indices, #gates)
+  int64_t alpha_base_gates = 0;             // #terms before the gate terms (Vanishing.hs:67-72)
+  int64_t n_pp_terms_per_round = 0, n_lookup_terms_per_round = 0;
+  Layout L;
+  int64_t trace_words = 0;
+};
+
+Circuit parse_circuit(const JVal& common, const JVal& vkey);   // throws ParseError / CircuitError
+void pack_proof(const Circuit& c, const JVal& proof, uint64_t* dst);   // throws ParseError / ShapeError
+GateDesc parse_gate_string(const std::string& s);              // Gate/Parser.hs:107-130
+
+}  // namespace p2v

@@ -1,0 +1,82 @@
+// dev.h — POD circuit descriptor passed by value to every kernel, plus the device-side
+// scratch layout.  All proofs of a batch share one circuit, so every shape below is
+// wave-uniform; the lane index is the proof index (SoA layout [word][B]).
+#pragma once
+#include <stdint.h>
+
+#define P2V_MAX_STEPS 8
+#define P2V_MAX_R 4
+
+struct DevCircuit {
+  int32_t B;            // lane stride (batch padded to a multiple of 64)
+  int32_t n;            // proofs in this run
+  int32_t r, Q, S, T;   // challenges, queries, FRI steps, trees per query (4 + S)
+  int32_t num_pis, cap_len, degree_bits, lde_bits, pow_bits;
+  int32_t num_wires, num_routed, num_constants, ngc, ngroups, nls, nlp, npp, qdf, nluts;
+  int32_t depth0, final_len;
+  int32_t arity[P2V_MAX_STEPS], step_depth[P2V_MAX_STEPS], step_logn[P2V_MAX_STEPS];
+  int32_t width[4];
+  int32_t n_gates;                 // gates evaluated = min(#selector_indices, #gates)
+  int32_t n_pp_terms, n_lookup_terms;
+  int64_t alpha_base_gates;
+  // packed layout (u64 word offsets)
+  int64_t pis, wcap, zcap, qcap, o_const, o_sig, o_wires, o_zs, o_pp, o_quot, o_lzs, o_zs_next, o_lzs_next;
+  int64_t n_this, n_next, ccaps, final_poly, pow, q0, qstride;
+  int64_t leaf[4], path[4], step_evals[P2V_MAX_STEPS], step_path[P2V_MAX_STEPS];
+  int64_t words;
+  // small constant tables
+  uint64_t digest[4];
+  uint64_t root_pow2[33];          // TWO_ADIC_GEN^(2^m): subgroup_gen(k)^(2^j) = root_pow2[32-k+j]
+  uint64_t step_shift[P2V_MAX_STEPS + 1];     // MULT_GEN^(prod of earlier arities)
+  uint64_t step_shift_inv[P2V_MAX_STEPS + 1];
+  uint64_t inv_arity[P2V_MAX_STEPS];          // 1 / 2^arity
+  // device tables
+  const uint64_t* cs_cap;          // [cap_len][4]
+  const uint64_t* k_is;            // [num_routed]
+  const int32_t* gate_kind;        // [n_gates]
+  const int64_t* gate_par;         // [n_gates][3]
+  const int32_t* gate_grp;         // [n_gates] selector group
+  const int32_t* gate_woff;        // [n_gates] offset into weights
+  const uint64_t* weights;         // CosetInterpolation barycentric weights
+  const int32_t* grp_start;        // [ngroups]
+  const int32_t* grp_end;
+  const uint64_t* lut_in;          // concatenated LUTs
+  const uint64_t* lut_out;
+  const int64_t* lut_off;          // [nluts]
+  const int64_t* lut_len;
+  const uint64_t* twiddles;        // per step: omega_{a}^{-j}, j < 2^a  (offset 256*s)
+  const int32_t* tops;             // transcript op program [ntops][3] (see TOP_*)
+  int32_t ntops;
+  // batch buffers
+  const uint64_t* soa;             // [words][B]
+  uint64_t* chal;                  // [CH_WORDS][B]
+  uint64_t* leafdig;               // [Q][T][4][B]
+  uint8_t* mk_ok;                  // [Q][T][B]
+  uint32_t* fri_bits;              // [Q][B]: bit s = step-s evaluation check, bit 31 = final check
+  uint64_t* qvals;                 // [Q][6][B]: initial, folded, final (F^2 each)
+  uint64_t* van;                   // [1 + 4r][B]: eqs_ok, C_i, quotient_i
+};
+
+// transcript op program (built on the host from the circuit; uniform across the batch)
+#define TOP_ABSORB_SOA 0    // absorb n words of the proof (SoA) from word a
+#define TOP_ABSORB_CHAL 1   // absorb n words of the challenge buffer from word a
+#define TOP_ABSORB_DIGEST 2 // absorb the circuit digest (n = 4)
+#define TOP_SQUEEZE 3       // squeeze n words into challenge words a..
+#define TOP_SQUEEZE_IDX 4   // squeeze n query indices (mod 2^lde_bits) into a..
+#define TOP_COPY 5          // challenge words a..a+n = words a-3r..  (lookup deltas := betas ++ gammas)
+#define TOP_ZERO 6          // challenge words a..a+n = 0
+
+// challenge buffer offsets (match the P2V_TRACE layout prefix in include/p2v.h)
+#define CH_PI(c) 0
+#define CH_BETA(c) 4
+#define CH_GAMMA(c) (4 + (c).r)
+#define CH_ALPHA(c) (4 + 2 * (c).r)
+#define CH_DELTA(c) (4 + 3 * (c).r)
+#define CH_ZETA(c) (4 + 7 * (c).r)
+#define CH_FRI_ALPHA(c) (CH_ZETA(c) + 2)
+#define CH_FRI_BETA(c) (CH_FRI_ALPHA(c) + 2)
+#define CH_POW(c) (CH_FRI_BETA(c) + 2 * (c).S)
+#define CH_QIDX(c) (CH_POW(c) + 1)
+#define CH_Y0(c) (CH_QIDX(c) + (c).Q)
+#define CH_Y1(c) (CH_Y0(c) + 2)
+#define CH_WORDS(c) (CH_Y1(c) + 2)

@@ -1,0 +1,109 @@
+// devcommon.h — device helpers shared by the verifier kernels.
+#pragma once
+#include "gl.h"
+#include "poseidon.h"
+#include "dev.h"
+
+namespace p2d {
+
+using gl::E;
+
+__device__ __forceinline__ uint64_t ld(const DevCircuit& c, int64_t w, int p) { return c.soa[w * c.B + p]; }
+__device__ __forceinline__ E lde(const DevCircuit& c, int64_t w, int p) { return E{ld(c, w, p), ld(c, w + 1, p)}; }
+__device__ __forceinline__ uint64_t& chal(const DevCircuit& c, int64_t w, int p) { return c.chal[w * c.B + p]; }
+__device__ __forceinline__ E chal_e(const DevCircuit& c, int64_t w, int p) { return E{c.chal[w * c.B + p], c.chal[(w + 1) * c.B + p]}; }
+
+// subgroup_gen(k)^e  (Goldilocks.hs:68-74): product of the precomputed 2^j-th powers.
+// e may differ per lane: multiply by 1 where the bit is clear (no divergence).
+__device__ __forceinline__ uint64_t pow_root(const DevCircuit& c, int k, uint32_t e) {
+  uint64_t acc = 1;
+  for (int j = 0; j < k; j++) {
+    uint64_t f = ((e >> j) & 1u) ? c.root_pow2[32 - k + j] : 1ULL;
+    acc = gl::mul(acc, f);
+  }
+  return acc;
+}
+
+// x^(p-2) by an addition chain (64 squarings + 9 multiplies); inv(0) = 0 like the
+// reference's pow-based inverse (Goldilocks.hs:155-156).
+__device__ __forceinline__ uint64_t sqn(uint64_t v, int n) { for (int i = 0; i < n; i++) v = gl::mul(v, v); return v; }
+__device__ __forceinline__ uint64_t inv_chain(uint64_t x) {
+  uint64_t e2 = gl::mul(gl::mul(x, x), x);
+  uint64_t e3 = gl::mul(gl::mul(e2, e2), x);
+  uint64_t e6 = gl::mul(sqn(e3, 3), e3);
+  uint64_t e12 = gl::mul(sqn(e6, 6), e6);
+  uint64_t e24 = gl::mul(sqn(e12, 12), e12);
+  uint64_t e30 = gl::mul(sqn(e24, 6), e6);
+  uint64_t e31 = gl::mul(gl::mul(e30, e30), x);
+  uint64_t z = gl::mul(gl::mul(e31, e31), x);
+  return gl::mul(sqn(e31, 33), z);
+}
+__device__ __forceinline__ uint64_t norm(E x) { return gl::sub(gl::mul(x.a, x.a), gl::mul_small(gl::mul(x.b, x.b), 7)); }
+__device__ __forceinline__ E einv(E x) {   // invExt, GoldilocksExt.hs:76-80
+  uint64_t d = inv_chain(norm(x));
+  return E{gl::mul(x.a, d), gl::mul(gl::neg(x.b), d)};
+}
+// 1/u and 1/v with one base-field inversion; exact inv(0)=0 semantics kept by a fallback
+__device__ __forceinline__ void einv2(E u, E v, E& iu, E& iv) {
+  uint64_t nu = norm(u), nv = norm(v);
+  uint64_t nuv = gl::mul(nu, nv);
+  if (nuv != 0) {
+    uint64_t t = inv_chain(nuv);
+    uint64_t inu = gl::mul(t, nv), inv_ = gl::mul(t, nu);
+    iu = E{gl::mul(u.a, inu), gl::mul(gl::neg(u.b), inu)};
+    iv = E{gl::mul(v.a, inv_), gl::mul(gl::neg(v.b), inv_)};
+  } else {
+    iu = einv(u); iv = einv(v);
+  }
+}
+__device__ __forceinline__ E epow_u(E x, uint32_t e) {   // uniform small exponent
+  E acc = gl::eb(1), s = x;
+  while (e) { if (e & 1) acc = gl::emul(acc, s); s = gl::emul(s, s); e >>= 1; }
+  return acc;
+}
+__device__ __forceinline__ E epow2n(E x, int n) { for (int i = 0; i < n; i++) x = gl::emul(x, x); return x; }
+
+// ---------------------------------------------------------------- state word access
+// uniform index into the 12-word register state (scalar branch, no scratch)
+__device__ __forceinline__ void st_set(uint64_t s[12], int i, uint64_t x) {
+  switch (i) {
+    case 0: s[0] = x; break; case 1: s[1] = x; break; case 2: s[2] = x; break; case 3: s[3] = x; break;
+    case 4: s[4] = x; break; case 5: s[5] = x; break; case 6: s[6] = x; break; case 7: s[7] = x; break;
+    default: break;
+  }
+}
+__device__ __forceinline__ uint64_t st_get(const uint64_t s[12], int i) {
+  switch (i) {
+    case 0: return s[0]; case 1: return s[1]; case 2: return s[2]; case 3: return s[3];
+    case 4: return s[4]; case 5: return s[5]; case 6: return s[6]; default: return s[7];
+  }
+}
+
+// Fiat–Shamir duplex in overwrite mode (Challenge/Pure.hs:27-107).  Buffered inputs are
+// written straight into the rate part of the state: nothing reads those words before the
+// duplex that would overwrite them, so permute(state) == duplex inp old.
+struct Duplex {
+  uint64_t s[12];
+  int nbuf;      // inputs buffered since the last duplex (uniform)
+  int outpos;    // next output word while squeezing (uniform), -1 = exhausted
+  bool absorbing;
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int i = 0; i < 12; i++) s[i] = 0;
+    nbuf = 0; outpos = -1; absorbing = true;
+  }
+  __device__ __forceinline__ void absorb(uint64_t x) {
+    if (!absorbing) { absorbing = true; nbuf = 0; }
+    if (nbuf == 8) { p2::permute(s); nbuf = 0; }
+    st_set(s, nbuf, x);
+    nbuf++;
+  }
+  __device__ __forceinline__ uint64_t squeeze() {
+    if (absorbing || outpos < 0) { p2::permute(s); absorbing = false; outpos = 7; }
+    uint64_t v = st_get(s, outpos);
+    outpos--;
+    return v;
+  }
+};
+
+}  // namespace p2d

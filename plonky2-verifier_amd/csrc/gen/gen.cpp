@@ -393,7 +393,11 @@ Witness* make_witness(const Circuit& C, u64 seed) {
 }
 
 // ------------------------------------------------------------------ proof
-std::string make_proof(const Circuit& C, const Witness& W, u64 pi_seed) {
+// flags (malicious-prover modes for reject-path tests):
+//   1: corrupt the first FRI layer before committing   -> step-0 evaluation mismatch
+//   2: corrupt the last FRI layer (final poly truncated) -> final polynomial mismatch
+//   4: corrupt a quotient opening                        -> Plonk identity fails
+std::string make_proof(const Circuit& C, const Witness& W, u64 pi_seed, unsigned flags = 0) {
   Rng rg(pi_seed * 104729 + 5);
   const size_t M = (size_t)1 << C.lde_bits;
   const int r = C.r;
@@ -427,6 +431,7 @@ std::string make_proof(const Circuit& C, const Witness& W, u64 pi_seed) {
   for (int i = 0; i < r; i++) { o_zs.push_back(gl::eb(1)); o_zs_next.push_back(gl::eb(1)); }
   for (int i = 0; i < r * C.npp; i++) o_pp.push_back(gl::eb(1));
   for (int i = 0; i < r * C.qdf; i++) o_quot.push_back(gl::e0());
+  if (flags & 4) o_quot[0] = gl::eb(12345);
   for (int k = 0; k < r * C.nlp; k++) { o_lzs.push_back(eval_at(W.lzs_coeffs[k], zeta)); o_lzs_next.push_back(eval_at(W.lzs_coeffs[k], zeta_w)); }
   std::vector<E> b1, b2;
   for (auto* v : {&o_const, &o_sig, &o_wires, &o_zs, &o_pp, &o_quot, &o_lzs}) b1.insert(b1.end(), v->begin(), v->end());
@@ -477,6 +482,7 @@ std::string make_proof(const Circuit& C, const Witness& W, u64 pi_seed) {
   std::vector<Tree> step_trees;
   std::vector<std::vector<E>> layers;   // values of each layer (bit-reversed order)
   std::vector<E> betas_fri;
+  if (flags & 1) for (auto& x : cw) x = gl::eadd(x, gl::eb(1));   // not the committed polynomial's values
   layers.push_back(cw);
   u64 shift = gl::MULT_GEN; int logn = C.lde_bits;
   for (size_t s = 0; s < C.arities.size(); s++) {
@@ -516,6 +522,7 @@ std::string make_proof(const Circuit& C, const Witness& W, u64 pi_seed) {
     logn -= ab;
   }
   // final polynomial: values on shift*<eta_f> (bit-reversed) -> coefficients
+  if (flags & 2) { Rng cr(pi_seed + 77); for (auto& x : layers.back()) x = gl::eadd(x, gl::eb(cr.field())); }
   std::vector<E> fin = layers.back();
   size_t nf = fin.size();
   std::vector<E> nat(nf);
@@ -528,7 +535,7 @@ std::string make_proof(const Circuit& C, const Witness& W, u64 pi_seed) {
     E ck = gl::escale(gl::mul(inv_nf, sp), nat[k]);
     sp = gl::mul(sp, sinv);
     if (k < final_len) final_poly[k] = ck;
-    else if (!(ck.a == 0 && ck.b == 0)) throw std::runtime_error("generator: final polynomial has too high degree");
+    else if (!(ck.a == 0 && ck.b == 0) && !(flags & 7)) throw std::runtime_error("generator: final polynomial has too high degree");
   }
   d.absorb_e(final_poly);
   // proof of work: find w s.t. the top pow_bits of the squeezed response are zero
@@ -621,6 +628,9 @@ void* p2v_gen_witness_new(void* c, uint64_t seed) {
 void p2v_gen_witness_free(void* w) { delete (Witness*)w; }
 char* p2v_gen_proof_json(void* c, void* w, uint64_t pi_seed) {
   try { return dupstr(make_proof(*(Circuit*)c, *(Witness*)w, pi_seed)); } catch (std::exception& e) { g_err = e.what(); return nullptr; }
+}
+char* p2v_gen_proof_json_flags(void* c, void* w, uint64_t pi_seed, unsigned flags) {
+  try { return dupstr(make_proof(*(Circuit*)c, *(Witness*)w, pi_seed, flags)); } catch (std::exception& e) { g_err = e.what(); return nullptr; }
 }
 void p2v_gen_free_str(char* s) { free(s); }
 const char* p2v_gen_last_error(void) { return g_err.c_str(); }

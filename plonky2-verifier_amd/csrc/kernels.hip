@@ -1,0 +1,360 @@
+// kernels.hip — gfx950 kernels of the batch verifier (everything except the vanishing /
+// gate-constraint kernel, which lives in vanish.hip).
+//
+// Data layout: the packed proofs are transposed once into SoA ([word][B], B = batch padded
+// to 64), so in every kernel lane i of a wave handles proof (64*pb + i) and all other
+// indices (query, tree, step, word) are wave-uniform: loads are fully coalesced 512-B rows,
+// control flow never diverges, and the Poseidon round constants are scalar operands.
+//
+//   k_transpose   proof-major -> SoA
+//   k_phase1      transcript waves (one lane per proof, ~114 sequential permutations,
+//                 Challenge/Verifier.hs:58-103 + Challenge/FRI.hs:65-104) run in the SAME
+//                 launch as the leaf-hash waves (one lane per (proof, query, tree) sponge,
+//                 Hash/Sponge.hs:26-31) which do not depend on the challenges
+//   k_merkle      path compression (Hash/Merkle.hs:27-42) for the 4 initial trees and every
+//                 FRI step tree, one lane per (proof, query, tree)
+//   k_fri         combineInitial + folding steps + final polynomial, one lane per
+//                 (proof, query)  (Plonk/FRI.hs:151-407)
+//   k_status      reference evaluation order -> int8 status (+ optional trace)
+#include "devcommon.h"
+
+using namespace p2d;
+using gl::E;
+
+// ------------------------------------------------------------------------ transpose
+extern "C" __global__ void __launch_bounds__(256) k_transpose(const uint64_t* __restrict__ in, int64_t words, int n,
+                                                              uint64_t* __restrict__ out, int B) {
+  __shared__ uint64_t tile[64][65];
+  const int64_t w0 = (int64_t)blockIdx.x * 64;
+  const int p0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;   // 64 x 4
+  for (int k = ty; k < 64; k += 4) {
+    int p = p0 + k; int64_t w = w0 + tx;
+    tile[k][tx] = (p < n && w < words) ? in[(int64_t)p * words + w] : 0;
+  }
+  __syncthreads();
+  for (int k = ty; k < 64; k += 4) {
+    int64_t w = w0 + k; int p = p0 + tx;
+    if (w < words) out[w * B + p] = tile[tx][k];
+  }
+}
+
+// ------------------------------------------------------------------------ helpers
+__device__ __forceinline__ void leaf_hash_unit(const DevCircuit& c, int unit, int lane) {
+  const int NPB = c.B >> 6;
+  const int pb = unit % NPB, qt = unit / NPB;
+  const int q = qt / c.T, t = qt % c.T;
+  const int p = pb * 64 + lane;
+  const int64_t base = c.q0 + (int64_t)q * c.qstride;
+  int64_t off; int len;
+  if (t < 4) { off = base + c.leaf[t]; len = c.width[t]; }
+  else { int s = t - 4; off = base + c.step_evals[s]; len = 2 << c.arity[s]; }
+  uint64_t st[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) st[i] = 0;
+  for (int i = 0; i < len; i += 8) {   // sponge, overwrite mode, no padding
+    const int k = len - i;
+#pragma unroll
+    for (int j = 0; j < 8; j++) if (j < k) st[j] = ld(c, off + i + j, p);
+    p2::permute(st);
+  }
+  uint64_t* dst = c.leafdig + ((int64_t)(q * c.T + t) * 4) * c.B + p;
+#pragma unroll
+  for (int i = 0; i < 4; i++) dst[(int64_t)i * c.B] = st[i];
+}
+
+// The transcript (Challenge/Verifier.hs:58-103, Challenge/FRI.hs:65-104) is a fixed
+// sequence of absorbs and squeezes for a given circuit; the host compiles it into an op
+// program and this loop interprets it with ONE permutation call site (the code size of
+// an inlined permutation is ~3k instructions).
+__device__ __forceinline__ void transcript_lane(const DevCircuit& c, int p) {
+  // public inputs hash, Hash/Sponge.hs:26-31 (sponge [] = zero digest)
+  {
+    uint64_t st[12];
+#pragma unroll
+    for (int i = 0; i < 12; i++) st[i] = 0;
+    for (int i = 0; i < c.num_pis; i += 8) {
+      const int k = c.num_pis - i;
+#pragma unroll
+      for (int j = 0; j < 8; j++) if (j < k) st[j] = ld(c, c.pis + i + j, p);
+      p2::permute(st);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) chal(c, CH_PI(c) + i, p) = st[i];
+  }
+  uint64_t s[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) s[i] = 0;
+  int nbuf = 0, outpos = -1;
+  bool absorbing = true;
+  const uint64_t qmask = (1ULL << c.lde_bits) - 1;
+  for (int o = 0; o < c.ntops; o++) {
+    const int type = c.tops[3 * o], a = c.tops[3 * o + 1], n = c.tops[3 * o + 2];
+    if (type == TOP_COPY) {   // mkLookupDeltaList (betas ++ gammas ++ ...), Challenge/Verifier.hs:36-40,82-86
+      for (int k = 0; k < n; k++) chal(c, a + k, p) = chal(c, a - 3 * c.r + k, p);
+      continue;
+    }
+    if (type == TOP_ZERO) {
+      for (int k = 0; k < n; k++) chal(c, a + k, p) = 0;
+      continue;
+    }
+    const bool ab = type <= TOP_ABSORB_DIGEST;
+    for (int k = 0; k < n; k++) {
+      uint64_t x = 0;
+      if (type == TOP_ABSORB_SOA) x = ld(c, (int64_t)a + k, p);
+      else if (type == TOP_ABSORB_CHAL) x = chal(c, a + k, p);
+      else if (type == TOP_ABSORB_DIGEST) x = c.digest[k & 3];
+      bool need;
+      if (ab) { if (!absorbing) { absorbing = true; nbuf = 0; } need = nbuf == 8; }
+      else need = absorbing || outpos < 0;
+      if (need) p2::permute(s);   // duplex / re-permute, Challenge/Pure.hs:38-69
+      if (ab) {
+        if (need) nbuf = 0;
+        st_set(s, nbuf, x);   // overwrite mode: input lands in the rate part
+        nbuf++;
+      } else {
+        if (need) { absorbing = false; outpos = 7; }
+        uint64_t v = st_get(s, outpos);   // output order state[7], state[6], ... (reverse of take 8)
+        outpos--;
+        if (type == TOP_SQUEEZE_IDX) v &= qmask;
+        chal(c, a + k, p) = v;
+      }
+    }
+  }
+  // precomputeReducedOpenings, Plonk/FRI.hs:128-134: Y = sum alpha^i y_i (Horner from the end)
+  const E alpha = chal_e(c, CH_FRI_ALPHA(c), p);
+  E y0 = gl::e0(), y1 = gl::e0();
+  for (int64_t i = c.n_this - 1; i >= 0; i--) y0 = gl::eadd(gl::emul(y0, alpha), lde(c, c.o_const + 2 * i, p));
+  for (int64_t i = c.n_next - 1; i >= 0; i--) y1 = gl::eadd(gl::emul(y1, alpha), lde(c, c.o_zs_next + 2 * i, p));
+  chal(c, CH_Y0(c), p) = y0.a; chal(c, CH_Y0(c) + 1, p) = y0.b;
+  chal(c, CH_Y1(c), p) = y1.a; chal(c, CH_Y1(c) + 1, p) = y1.b;
+}
+
+// ------------------------------------------------------------------------ phase 1
+// blocks [0, nt_blocks): transcript (4 waves x 64 proofs); the rest: leaf hashing, 4 units
+// per block.  Transcript blocks come first so their long serial chains start early.
+extern "C" __global__ void __launch_bounds__(256) k_phase1(DevCircuit c, int nt_blocks) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if ((int)blockIdx.x < nt_blocks) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p < c.B) transcript_lane(c, p);
+    return;
+  }
+  const int unit = ((int)blockIdx.x - nt_blocks) * 4 + wave;
+  const int units = c.Q * c.T * (c.B >> 6);
+  if (unit < units) leaf_hash_unit(c, unit, lane);
+}
+
+// ------------------------------------------------------------------------ Merkle paths
+extern "C" __global__ void __launch_bounds__(256) k_merkle(DevCircuit c) {
+  const int lane = threadIdx.x & 63;
+  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int NPB = c.B >> 6;
+  if (unit >= c.Q * c.T * NPB) return;
+  const int pb = unit % NPB, qt = unit / NPB;
+  const int q = qt / c.T, t = qt % c.T;
+  const int p = pb * 64 + lane;
+  const int64_t base = c.q0 + (int64_t)q * c.qstride;
+  uint32_t idx = (uint32_t)chal(c, CH_QIDX(c) + q, p);
+  int depth; int64_t poff;
+  if (t < 4) { depth = c.depth0; poff = base + c.path[t]; }
+  else {
+    const int s = t - 4;
+    int sh = 0;
+    for (int j = 0; j <= s; j++) sh += c.arity[j];
+    idx >>= sh; depth = c.step_depth[s]; poff = base + c.step_path[s];
+  }
+  const uint64_t* src = c.leafdig + ((int64_t)(q * c.T + t) * 4) * c.B + p;
+  uint64_t cur[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) cur[i] = src[(int64_t)i * c.B];
+  for (int l = 0; l < depth; l++) {   // even index: compress(cur, sib), odd: compress(sib, cur)
+    uint64_t sib[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) sib[i] = ld(c, poff + 4 * l + i, p);
+    const bool odd = idx & 1u;
+    uint64_t st[12];
+#pragma unroll
+    for (int i = 0; i < 4; i++) { st[i] = odd ? sib[i] : cur[i]; st[4 + i] = odd ? cur[i] : sib[i]; st[8 + i] = 0; }
+    p2::permute(st);
+#pragma unroll
+    for (int i = 0; i < 4; i++) cur[i] = st[i];
+    idx >>= 1;
+  }
+  // cap_roots !! (idx >> depth)
+  bool ok = idx < (uint32_t)c.cap_len;
+  const uint32_t ci = ok ? idx : 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint64_t root;
+    if (t == 0) root = c.cs_cap[ci * 4 + i];
+    else if (t == 1) root = ld(c, c.wcap + ci * 4 + i, p);
+    else if (t == 2) root = ld(c, c.zcap + ci * 4 + i, p);
+    else if (t == 3) root = ld(c, c.qcap + ci * 4 + i, p);
+    else root = ld(c, c.ccaps + (int64_t)(t - 4) * 4 * c.cap_len + ci * 4 + i, p);
+    ok = ok && (root == cur[i]);
+  }
+  c.mk_ok[(int64_t)(q * c.T + t) * c.B + p] = ok ? 1 : 0;
+}
+
+// ------------------------------------------------------------------------ FRI query
+// foldCosetWith (Plonk/FRI.hs:263-279) for arity 2^AB: the coset values (received order v,
+// bit-reversed coset order vals[rev k] = v[k]) are interpolated and evaluated at beta.
+// c_k = sum_j vals_j w^{-jk} is a DIT FFT applied to v directly (v is already the
+// bit-reversal of vals); P(beta) = (1/2^AB) sum_k c_k (beta/ofs)^k.
+template <int AB>
+__device__ __forceinline__ E fold_regs(const DevCircuit& c, int s, int64_t off, int p, E beta_over_ofs) {
+  constexpr int AR = 1 << AB;
+  E a[AR];
+#pragma unroll
+  for (int k = 0; k < AR; k++) a[k] = lde(c, off + 2 * k, p);
+  const uint64_t* tw = c.twiddles + 256 * s;   // omega^{-j}
+#pragma unroll
+  for (int len = 2; len <= AR; len <<= 1) {
+#pragma unroll
+    for (int i = 0; i < AR; i += len) {
+#pragma unroll
+      for (int k = 0; k < len / 2; k++) {
+        E u = a[i + k], v = a[i + k + len / 2];
+        if (k != 0) v = gl::escale(tw[k * (AR / len)], v);
+        a[i + k] = gl::eadd(u, v);
+        a[i + k + len / 2] = gl::esub(u, v);
+      }
+    }
+  }
+  E acc = gl::e0();
+#pragma unroll
+  for (int k = AR - 1; k >= 0; k--) acc = gl::eadd(gl::emul(acc, beta_over_ofs), a[k]);
+  return gl::escale(c.inv_arity[s], acc);
+}
+// generic arity: direct O(arity^2) evaluation of the same interpolant
+__device__ E fold_generic(const DevCircuit& c, int s, int ab, int64_t off, int p, E beta_over_ofs) {
+  const int ar = 1 << ab;
+  const uint64_t* tw = c.twiddles + 256 * s;
+  E acc = gl::e0();
+  for (int k = ar - 1; k >= 0; k--) {
+    E ck = gl::e0();
+    for (int j = 0; j < ar; j++) {
+      const int jj = (int)gl::rev_bits(ab, (uint32_t)j);   // vals[j] = v[rev j]
+      ck = gl::eadd(ck, gl::escale(tw[(j * k) & (ar - 1)], lde(c, off + 2 * jj, p)));
+    }
+    acc = gl::eadd(gl::emul(acc, beta_over_ofs), ck);
+  }
+  return gl::escale(c.inv_arity[s], acc);
+}
+
+extern "C" __global__ void __launch_bounds__(256) k_fri(DevCircuit c) {
+  const int lane = threadIdx.x & 63;
+  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int NPB = c.B >> 6;
+  if (unit >= c.Q * NPB) return;
+  const int pb = unit % NPB, q = unit / NPB;
+  const int p = pb * 64 + lane;
+  const int64_t base = c.q0 + (int64_t)q * c.qstride;
+  const int r = c.r;
+  uint32_t idx = (uint32_t)chal(c, CH_QIDX(c) + q, p);
+  const E alpha = chal_e(c, CH_FRI_ALPHA(c), p);
+  const E zeta = chal_e(c, CH_ZETA(c), p);
+  // combineInitial, Plonk/FRI.hs:151-207.  firstBatch = consts|sigmas, wires, pp part,
+  // quotient, lookup part; secondBatch = first r of the pp part, lookup part.
+  const int npp_all = r * ((c.num_routed + c.qdf - 1) / c.qdf);
+  const int64_t l0 = base + c.leaf[0], l1 = base + c.leaf[1], l2 = base + c.leaf[2], l3 = base + c.leaf[3];
+  E g0 = gl::e0(), g1 = gl::e0();
+  for (int i = c.width[2] - 1; i >= npp_all; i--) g0 = gl::eadd(gl::emul(g0, alpha), gl::eb(ld(c, l2 + i, p)));
+  for (int i = c.width[3] - 1; i >= 0; i--) g0 = gl::eadd(gl::emul(g0, alpha), gl::eb(ld(c, l3 + i, p)));
+  for (int i = npp_all - 1; i >= 0; i--) g0 = gl::eadd(gl::emul(g0, alpha), gl::eb(ld(c, l2 + i, p)));
+  for (int i = c.width[1] - 1; i >= 0; i--) g0 = gl::eadd(gl::emul(g0, alpha), gl::eb(ld(c, l1 + i, p)));
+  for (int i = c.width[0] - 1; i >= 0; i--) g0 = gl::eadd(gl::emul(g0, alpha), gl::eb(ld(c, l0 + i, p)));
+  for (int i = c.width[2] - 1; i >= npp_all; i--) g1 = gl::eadd(gl::emul(g1, alpha), gl::eb(ld(c, l2 + i, p)));
+  for (int i = (r < npp_all ? r : npp_all) - 1; i >= 0; i--) g1 = gl::eadd(gl::emul(g1, alpha), gl::eb(ld(c, l2 + i, p)));
+  const int len2 = (r < npp_all ? r : npp_all) + (c.width[2] - npp_all);
+  const uint64_t px = gl::mul(gl::MULT_GEN, pow_root(c, c.lde_bits, gl::rev_bits(c.lde_bits, idx)));
+  const uint64_t omega = c.root_pow2[32 - c.degree_bits];
+  E d0 = gl::esub(gl::eb(px), zeta), d1 = gl::esub(gl::eb(px), gl::escale(omega, zeta));
+  E i0, i1; einv2(d0, d1, i0, i1);
+  const E one = gl::emul(gl::esub(g0, chal_e(c, CH_Y0(c), p)), i0);
+  const E two = gl::emul(gl::esub(g1, chal_e(c, CH_Y1(c), p)), i1);
+  E cur = gl::eadd(gl::emul(epow_u(alpha, (uint32_t)len2), one), two);
+  uint64_t* qv = c.qvals + (int64_t)q * 6 * c.B + p;
+  qv[0] = cur.a; qv[(int64_t)c.B] = cur.b;
+  // folding steps, Plonk/FRI.hs:306-323
+  uint32_t bits = 0;
+  int logn = c.lde_bits;
+  for (int s = 0; s < c.S; s++) {
+    const int ab = c.arity[s];
+    const int64_t eoff = base + c.step_evals[s];
+    const uint32_t pos = idx & ((1u << ab) - 1);
+    const E at = lde(c, eoff + 2 * pos, p);   // evals !! (idx mod arity)
+    if (gl::eeq(at, cur)) bits |= 1u << s;
+    // coset offset shift * eta^{rev((idx >> a) << a)}, and its inverse without an inversion
+    const uint32_t start = gl::rev_bits(logn, (idx >> ab) << ab);
+    const uint32_t nmask = (logn >= 32) ? 0xFFFFFFFFu : ((1u << logn) - 1);
+    const uint64_t ofs_inv = gl::mul(c.step_shift_inv[s], pow_root(c, logn, (0u - start) & nmask));
+    const E beta = chal_e(c, CH_FRI_BETA(c) + 2 * s, p);
+    const E bo = gl::escale(ofs_inv, beta);
+    E nv;
+    switch (ab) {
+      case 1: nv = fold_regs<1>(c, s, eoff, p, bo); break;
+      case 2: nv = fold_regs<2>(c, s, eoff, p, bo); break;
+      case 3: nv = fold_regs<3>(c, s, eoff, p, bo); break;
+      case 4: nv = fold_regs<4>(c, s, eoff, p, bo); break;
+      default: nv = fold_generic(c, s, ab, eoff, p, bo); break;
+    }
+    cur = nv;
+    idx >>= ab; logn -= ab;
+  }
+  qv[2 * (int64_t)c.B] = cur.a; qv[3 * (int64_t)c.B] = cur.b;
+  // final polynomial at x = shift * eta^{rev idx}, Plonk/FRI.hs:288-291,325-327
+  const uint64_t xf = gl::mul(c.step_shift[c.S], pow_root(c, logn, gl::rev_bits(logn, idx)));
+  E acc = gl::e0();
+  for (int k = c.final_len - 1; k >= 0; k--) acc = gl::eadd(gl::escale(xf, acc), lde(c, c.final_poly + 2 * k, p));
+  qv[4 * (int64_t)c.B] = acc.a; qv[5 * (int64_t)c.B] = acc.b;
+  if (gl::eeq(acc, cur)) bits |= 1u << 31;
+  c.fri_bits[(int64_t)q * c.B + p] = bits;
+}
+
+// ------------------------------------------------------------------------ status
+// verifyProof = eqs_ok && (pow_ok && and [rounds in order]) with the reference's error
+// precedence inside a round (Plonk/Verifier.hs:62, Plonk/FRI.hs:370-407, 105-117, 306-313).
+extern "C" __global__ void __launch_bounds__(256) k_status(DevCircuit c, int8_t* __restrict__ results, uint64_t* __restrict__ trace,
+                                                           int64_t trace_words) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= c.n) return;
+  const bool eqs_ok = c.van[p] != 0;
+  const uint64_t resp = chal(c, CH_POW(c), p);
+  const int pb = c.pow_bits;
+  const uint64_t mask = pb <= 0 ? 0ULL : (pb >= 64 ? ~0ULL : (((1ULL << pb) - 1) << (64 - pb)));
+  const bool pow_ok = (resp & mask) == 0;
+  int8_t st = 1;
+  if (!eqs_ok || !pow_ok) st = 0;
+  else {
+    for (int q = 0; q < c.Q && st == 1; q++) {
+      const uint8_t* mk = c.mk_ok + (int64_t)q * c.T * c.B + p;
+      bool init_ok = mk[0] && mk[c.B] && mk[2 * (int64_t)c.B] && mk[3 * (int64_t)c.B];
+      if (!init_ok) { st = -1; break; }
+      const uint32_t bits = c.fri_bits[(int64_t)q * c.B + p];
+      for (int s = 0; s < c.S; s++) {
+        if (!mk[(int64_t)(4 + s) * c.B]) { st = -2; break; }
+        if (!((bits >> s) & 1u)) { st = -3; break; }
+      }
+      if (st != 1) break;
+      if (!((bits >> 31) & 1u)) st = 0;
+    }
+  }
+  results[p] = st;
+  if (trace) {
+    uint64_t* tr = trace + (int64_t)p * trace_words;
+    const int r = c.r, S = c.S, Q = c.Q;
+    int64_t k = 0;
+    for (int64_t w = 0; w < CH_QIDX(c) + Q; w++) tr[k++] = chal(c, w, p);
+    for (int i = 0; i < 4 * r; i++) tr[k++] = c.van[(int64_t)(1 + i) * c.B + p];   // C_i then quotient_i
+    for (int j = 0; j < 3; j++)
+      for (int q = 0; q < Q; q++) {
+        const uint64_t* qv = c.qvals + (int64_t)q * 6 * c.B + p;
+        tr[k++] = qv[(int64_t)(2 * j) * c.B];
+        tr[k++] = qv[(int64_t)(2 * j + 1) * c.B];
+      }
+    tr[k++] = (uint64_t)(eqs_ok ? 1 : 0) | ((uint64_t)(pow_ok ? 1 : 0) << 1);
+    (void)S;
+  }
+}

@@ -1,0 +1,5 @@
+// lib.hip — single translation unit for the device code + the C-ABI (kernels are launched
+// from the same TU that defines them; no relocatable device code needed).
+#include "kernels.hip"
+#include "vanish.hip"
+#include "api.cpp"

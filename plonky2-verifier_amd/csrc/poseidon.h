@@ -20,6 +20,13 @@ __host__ __device__ constexpr uint32_t mds_coeff(int i, int j) {
 
 #if defined(__HIPCC__)
 static __constant__ uint64_t c_round_constants[360] = P2V_ALL_ROUND_CONSTANTS_INIT;
+// fast partial-round tables, used only by the PoseidonGate constraint program
+// (Gate/Custom/Poseidon.hs:92-137, Hash/Constants.hs:27-113)
+static __constant__ uint64_t c_fast_first_rc[12] = P2V_FAST_PARTIAL_FIRST_ROUND_CONSTANT_INIT;
+static __constant__ uint64_t c_fast_rc[22] = P2V_FAST_PARTIAL_ROUND_CONSTANTS_INIT;
+static __constant__ uint64_t c_fast_vs[22 * 11] = P2V_FAST_PARTIAL_ROUND_VS_INIT;
+static __constant__ uint64_t c_fast_w_hats[22 * 11] = P2V_FAST_PARTIAL_ROUND_W_HATS_INIT;
+static __constant__ uint64_t c_fast_init_matrix[11 * 11] = P2V_FAST_PARTIAL_ROUND_INITIAL_MATRIX_INIT;
 #endif
 static const uint64_t h_round_constants[360] = P2V_ALL_ROUND_CONSTANTS_INIT;
 

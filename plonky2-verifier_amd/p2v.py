@@ -1,0 +1,290 @@
+"""p2v — host-side mirror of the reference verifier's API over libp2v (ctypes).
+
+The reference (bkomuves/plonky2-verifier, Haskell) exposes
+
+    verifyProof :: VerifierCircuitData -> ProofWithPublicInputs -> Bool   (src/Plonk/Verifier.hs:56)
+
+with inputs decoded from JSON by the Types.hs aeson instances (src/Types.hs:47-279).
+This module keeps that shape:
+
+    vkey  = VerifierCircuitData.from_json(common_json, vkey_json)      # Types.hs:220-224
+    proof = ProofWithPublicInputs.from_json(proof_json)                # Types.hs:245-254
+    ok    = verify_proof(vkey, proof)                                  # Plonk/Verifier.hs:56
+
+and adds the batch form the GPU is built for (verify_proof_batch / BatchVerifier).
+Where the reference raises `error` (failed Merkle proof, folding-step mismatch, shape
+mismatch, unsupported circuit) this module raises VerifierError with the same class;
+verify_proof returns False exactly where the reference returns False.
+
+All verification runs in libp2v's HIP kernels on MI355X; there is no CPU fallback — on a
+machine without a GPU, verification raises P2VError(P2V_E_NODEVICE).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Iterable, List, Optional, Sequence, Union
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libp2v.so")
+
+# per-proof status codes (include/p2v.h)
+ACCEPT = 1
+REJECT = 0
+ERR_INITIAL_MERKLE = -1
+ERR_STEP_MERKLE = -2
+ERR_STEP_EVAL = -3
+ERR_STEP_ARITY = -4
+ERR_SHAPE = -5
+ERR_CIRCUIT = -6
+ERR_PARSE = -7
+
+STATUS_MESSAGES = {
+    ERR_INITIAL_MERKLE: "checkInitialTreeProofs: at least one Merkle proof failed",   # Plonk/FRI.hs:108
+    ERR_STEP_MERKLE: "folding step Merkle proof does not check out",                  # Plonk/FRI.hs:310
+    ERR_STEP_EVAL: "folding step evaluation does not match the opening",              # Plonk/FRI.hs:311
+    ERR_STEP_ARITY: "folding stpe: reduction strategy incompatibility",               # Plonk/FRI.hs:312
+    ERR_SHAPE: "shape mismatch between proof and circuit",
+    ERR_CIRCUIT: "circuit not supported",
+    ERR_PARSE: "JSON did not decode",
+}
+
+# function return codes
+E_OK, E_PARSE, E_CIRCUIT, E_SHAPE, E_ARG, E_DEVICE, E_NODEVICE = 0, -1, -2, -3, -4, -5, -6
+
+FLAG_INPUT_DEVICE = 1
+FLAG_RESULT_DEVICE = 2
+FLAG_NO_SYNC = 4
+
+
+class P2VError(RuntimeError):
+    """A libp2v call failed (return code < 0)."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(f"libp2v error {code}: {message}")
+        self.code = code
+        self.message = message
+
+
+class VerifierError(RuntimeError):
+    """The reference verifier would raise `error` for this proof (status < 0)."""
+
+    def __init__(self, status: int):
+        super().__init__(STATUS_MESSAGES.get(status, f"status {status}"))
+        self.status = status
+
+
+class _Info(ctypes.Structure):
+    _fields_ = [
+        ("degree_bits", ctypes.c_int32), ("lde_bits", ctypes.c_int32), ("cap_height", ctypes.c_int32),
+        ("num_challenges", ctypes.c_int32), ("num_query_rounds", ctypes.c_int32), ("num_fri_steps", ctypes.c_int32),
+        ("final_poly_len", ctypes.c_int32), ("num_public_inputs", ctypes.c_int32), ("num_openings_this", ctypes.c_int32),
+        ("num_openings_next", ctypes.c_int32), ("has_lookups", ctypes.c_int32), ("num_gates", ctypes.c_int32),
+        ("proof_words", ctypes.c_int64), ("trace_words", ctypes.c_int64), ("oracle_widths", ctypes.c_int32 * 4),
+        ("step_arity_bits", ctypes.c_int32 * 8),
+    ]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libp2v.so (built in-tree by `make -C plonky2-verifier_amd`).  Fails loudly."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is not built; run `make -C {_HERE}` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, u64p, i8p = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p
+    L.p2v_circuit_from_json.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.POINTER(vp)]
+    L.p2v_circuit_free.argtypes = [vp]
+    L.p2v_circuit_free.restype = None
+    L.p2v_circuit_get_info.argtypes = [vp, ctypes.POINTER(_Info)]
+    L.p2v_pack_proof_json.argtypes = [vp, ctypes.c_char_p, sz, u64p]
+    L.p2v_device_count.argtypes = []
+    L.p2v_verifier_create.argtypes = [vp, ctypes.c_int, sz, ctypes.POINTER(vp)]
+    L.p2v_verifier_free.argtypes = [vp]
+    L.p2v_verifier_free.restype = None
+    L.p2v_verifier_run.argtypes = [vp, u64p, sz, i8p, u64p, vp, ctypes.c_uint32]
+    L.p2v_verify_batch.argtypes = [vp, u64p, sz, i8p, ctypes.c_int]
+    L.p2v_verifier_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+    L.p2v_kernel_names.restype = ctypes.c_char_p
+    L.p2v_last_error_message.restype = ctypes.c_char_p
+    L.p2v_version.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def _check(rc: int) -> None:
+    if rc != E_OK:
+        raise P2VError(rc, lib().p2v_last_error_message().decode(errors="replace"))
+
+
+def _bytes(x: Union[str, bytes]) -> bytes:
+    return x.encode() if isinstance(x, str) else bytes(x)
+
+
+@dataclass(frozen=True)
+class CircuitInfo:
+    degree_bits: int
+    lde_bits: int
+    cap_height: int
+    num_challenges: int
+    num_query_rounds: int
+    num_fri_steps: int
+    final_poly_len: int
+    num_public_inputs: int
+    num_openings_this: int
+    num_openings_next: int
+    has_lookups: bool
+    num_gates: int
+    proof_words: int
+    trace_words: int
+    oracle_widths: tuple
+    step_arity_bits: tuple
+
+
+class VerifierCircuitData:
+    """VerifierCircuitData = VerifierOnlyCircuitData + CommonCircuitData (Types.hs:220-224).
+
+    Decoding and every circuit-level check of the reference (unknown gate, selector
+    tally, unsupported reduction strategy, ...) happen once here (P2VError otherwise)."""
+
+    def __init__(self, handle: int):
+        self._h = ctypes.c_void_p(handle)
+        inf = _Info()
+        _check(lib().p2v_circuit_get_info(self._h, ctypes.byref(inf)))
+        self.info = CircuitInfo(
+            inf.degree_bits, inf.lde_bits, inf.cap_height, inf.num_challenges, inf.num_query_rounds, inf.num_fri_steps,
+            inf.final_poly_len, inf.num_public_inputs, inf.num_openings_this, inf.num_openings_next, bool(inf.has_lookups),
+            inf.num_gates, inf.proof_words, inf.trace_words, tuple(inf.oracle_widths), tuple(inf.step_arity_bits[: inf.num_fri_steps]))
+
+    @classmethod
+    def from_json(cls, common_json: Union[str, bytes], vkey_json: Union[str, bytes]) -> "VerifierCircuitData":
+        c, v = _bytes(common_json), _bytes(vkey_json)
+        h = ctypes.c_void_p()
+        _check(lib().p2v_circuit_from_json(c, len(c), v, len(v), ctypes.byref(h)))
+        return cls(h.value)
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def pack(self, proof_json: Union[str, bytes], out: Optional[np.ndarray] = None) -> np.ndarray:
+        """ProofWithPublicInputs JSON (Types.hs:245-254) -> packed u64 words of this circuit."""
+        b = _bytes(proof_json)
+        if out is None:
+            out = np.empty(self.info.proof_words, dtype=np.uint64)
+        assert out.dtype == np.uint64 and out.size == self.info.proof_words and out.flags.c_contiguous
+        _check(lib().p2v_pack_proof_json(self._h, b, len(b), out.ctypes.data))
+        return out
+
+    def pack_many(self, proofs: Sequence[Union[str, bytes]]) -> np.ndarray:
+        arr = np.empty((len(proofs), self.info.proof_words), dtype=np.uint64)
+        for i, p in enumerate(proofs):
+            self.pack(p, arr[i])
+        return arr
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None) and self._h.value:
+                lib().p2v_circuit_free(self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
+@dataclass
+class ProofWithPublicInputs:
+    """ProofWithPublicInputs (Types.hs:245-254), kept as JSON text until packed."""
+
+    json: bytes
+
+    @classmethod
+    def from_json(cls, text: Union[str, bytes]) -> "ProofWithPublicInputs":
+        return cls(_bytes(text))
+
+
+def device_count() -> int:
+    return int(lib().p2v_device_count())
+
+
+class BatchVerifier:
+    """A per-device workspace bound to one circuit (all device memory allocated here)."""
+
+    def __init__(self, circuit: VerifierCircuitData, device: int = 0, max_batch: int = 4096):
+        self.circuit = circuit
+        self.device = device
+        self.max_batch = max_batch
+        h = ctypes.c_void_p()
+        _check(lib().p2v_verifier_create(circuit.handle, device, max_batch, ctypes.byref(h)))
+        self._h = h
+
+    def run(self, proofs: np.ndarray, trace: bool = False):
+        """proofs: uint64 [n, proof_words] host array.  Returns int8 statuses (and trace)."""
+        proofs = np.ascontiguousarray(proofs, dtype=np.uint64)
+        n = proofs.shape[0]
+        res = np.empty(n, dtype=np.int8)
+        tr = np.empty((n, self.circuit.info.trace_words), dtype=np.uint64) if trace else None
+        _check(lib().p2v_verifier_run(self._h, proofs.ctypes.data, n, res.ctypes.data,
+                                      tr.ctypes.data if trace else None, None, 0))
+        return (res, tr) if trace else res
+
+    def run_device(self, proofs_ptr: int, n: int, results_ptr: int, stream: int = 0, trace_ptr: int = 0,
+                   sync: bool = True) -> None:
+        """Device-resident batch: raw device pointers (e.g. torch tensor .data_ptr()) and a
+        hipStream_t handle (torch.cuda.current_stream().cuda_stream)."""
+        flags = FLAG_INPUT_DEVICE | FLAG_RESULT_DEVICE | (0 if sync else FLAG_NO_SYNC)
+        _check(lib().p2v_verifier_run(self._h, ctypes.c_void_p(proofs_ptr), n, ctypes.c_void_p(results_ptr),
+                                      ctypes.c_void_p(trace_ptr) if trace_ptr else None, ctypes.c_void_p(stream), flags))
+
+    def last_timings(self) -> dict:
+        buf = (ctypes.c_float * 16)()
+        k = lib().p2v_verifier_last_timings(self._h, buf, 16)
+        names = lib().p2v_kernel_names().decode().split(",")
+        return {names[i]: float(buf[i]) for i in range(k)}
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None) and self._h.value:
+                lib().p2v_verifier_free(self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
+def _status_to_bool(st: int) -> bool:
+    if st == ACCEPT:
+        return True
+    if st == REJECT:
+        return False
+    raise VerifierError(int(st))
+
+
+def verify_proof(vkey: VerifierCircuitData, proof: Union[ProofWithPublicInputs, str, bytes], device: int = 0) -> bool:
+    """verifyProof (Plonk/Verifier.hs:56-65): True / False, or VerifierError where the
+    reference raises `error`."""
+    text = proof.json if isinstance(proof, ProofWithPublicInputs) else _bytes(proof)
+    packed = vkey.pack(text)[None, :]
+    res = np.empty(1, dtype=np.int8)
+    _check(lib().p2v_verify_batch(vkey.handle, packed.ctypes.data, 1, res.ctypes.data, device))
+    return _status_to_bool(int(res[0]))
+
+
+def verify_proof_batch(vkey: VerifierCircuitData, proofs: Iterable[Union[ProofWithPublicInputs, str, bytes]],
+                       device: int = 0) -> List[Union[bool, VerifierError]]:
+    """Batch form: one entry per proof, True/False or the VerifierError the reference would raise."""
+    texts = [p.json if isinstance(p, ProofWithPublicInputs) else _bytes(p) for p in proofs]
+    if not texts:
+        return []
+    packed = vkey.pack_many(texts)
+    res = np.empty(len(texts), dtype=np.int8)
+    _check(lib().p2v_verify_batch(vkey.handle, packed.ctypes.data, len(texts), res.ctypes.data, device))
+    out: List[Union[bool, VerifierError]] = []
+    for st in res:
+        out.append(True if st == ACCEPT else False if st == REJECT else VerifierError(int(st)))
+    return out
