@@ -288,3 +288,29 @@ def verify_proof_batch(vkey: VerifierCircuitData, proofs: Iterable[Union[ProofWi
     for st in res:
         out.append(True if st == ACCEPT else False if st == REJECT else VerifierError(int(st)))
     return out
+
+
+# ----------------------------------------------------------------------------- multi-GPU
+def shard_bounds(n: int, world: int, rank: int):
+    """Contiguous near-equal shard [start, end) of n proofs for `rank` of `world`.
+    Proofs are independent (verifyProof has no cross-proof state), so a batch shards
+    across GPUs with no collective on the data path."""
+    base, extra = divmod(n, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def verify_sharded(vkey: VerifierCircuitData, packed: np.ndarray, rank: int, world: int, device: int,
+                   group=None) -> np.ndarray:
+    """Each rank verifies its shard of `packed` on its own GPU; the int8 statuses are then
+    gathered so every rank holds the full result vector (one small all_gather of results,
+    the only cross-rank traffic)."""
+    import torch
+    import torch.distributed as dist
+    s, e = shard_bounds(packed.shape[0], world, rank)
+    local = BatchVerifier(vkey, device, max(1, e - s)).run(packed[s:e]) if e > s else np.empty(0, np.int8)
+    if world == 1:
+        return local
+    parts = [None] * world
+    dist.all_gather_object(parts, local.tolist(), group=group)
+    return np.array([x for p in parts for x in p], dtype=np.int8)

@@ -1,0 +1,65 @@
+"""Multi-process sharding (gloo, world_size 2, CPU): the proof-sharding and result
+gathering used for N GPUs (embarrassingly parallel, no data-path
+collective).  The per-shard verification here is the ORACLE (CPU) so the test runs
+without a GPU; on GPUs each rank runs libp2v on its own device."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from support import gen_circuit, oracle, p2v_module
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, proofs, common, vkey, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p2v = p2v_module()
+    s, e = p2v.shard_bounds(len(proofs), world, rank)
+    O = oracle()
+    local = [O.verify_json(common, vkey, proofs[i]) for i in range(s, e)]
+    parts = [None] * world
+    dist.all_gather_object(parts, local)
+    flat = [x for p in parts for x in p]
+    if rank == 0:
+        out.put(flat)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_bounds_cover_exactly():
+    p2v = p2v_module()
+    for n in (0, 1, 7, 64, 4097):
+        for w in (1, 2, 3, 8):
+            spans = [p2v.shard_bounds(n, w, r) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+            sizes = [e - s for s, e in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_two_rank_gloo_sharded_verification():
+    gc = gen_circuit(6, 4, 0)
+    proofs = [gc.proof(1, 1), gc.proof(1, 5, flags=2), gc.proof(2, 2), gc.proof(1, 4, flags=1), gc.proof(2, 3)]
+    expect = [oracle().verify_json(gc.common, gc.vkey, p) for p in proofs]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, proofs, gc.common, gc.vkey, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got == expect == [1, 0, 1, -3, 1]

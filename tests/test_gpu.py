@@ -1,0 +1,133 @@
+"""GPU parity tests (MI355X): libp2v's HIP path vs the ORACLE, bit-exact.
+
+Statuses and the full debug trace (challenges, pi hash, lookup deltas, zeta, FRI
+alpha/betas, PoW response, query indices, alpha-combined constraint values, quotient
+values, per-query combineInitial / folded / final-polynomial values) must equal the
+oracle's word for word.  Integer arithmetic: no tolerance anywhere."""
+import gzip
+import json
+import os
+
+import numpy as np
+import pytest
+
+from support import GOLDEN, gen_circuit, mutate, oracle, p2v_module
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def p2v():
+    m = p2v_module()
+    if m.device_count() == 0:
+        pytest.fail("no GPU visible to libp2v")
+    return m
+
+
+def _cases(gc):
+    from test_oracle import _reject_cases
+    out = [(gc.proof(w, s), 1) for w, s in ((1, 1), (2, 2), (1, 9))]
+    return out + _reject_cases(gc)
+
+
+@pytest.mark.parametrize("nb,lk", [(6, 0), (6, 1), (8, 0)])
+def test_gpu_matches_oracle_status_and_trace(p2v, nb, lk):
+    O = oracle()
+    gc = gen_circuit(nb, 4, lk)
+    cases = _cases(gc)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    bv = p2v.BatchVerifier(vk, 0, len(cases))
+    res, tr = bv.run(vk.pack_many([c[0] for c in cases]), trace=True)
+    for i, (proof, expect) in enumerate(cases):
+        st, otr = O.verify_json(gc.common, gc.vkey, proof, trace=True)
+        assert st == expect
+        assert res[i] == st, i
+        assert np.array_equal(tr[i], otr), (i, np.nonzero(tr[i] != otr)[0][:10])
+
+
+def test_gpu_golden_fixtures(p2v):
+    exp = json.load(open(os.path.join(GOLDEN, "expected.json")))["cases"]
+
+    def rd(n):
+        with gzip.open(os.path.join(GOLDEN, n), "rb") as f:
+            return f.read()
+    by_circ = {}
+    for c in exp:
+        by_circ.setdefault(c["circuit"], []).append(c)
+    for circ, cases in by_circ.items():
+        vk = p2v.VerifierCircuitData.from_json(rd(circ + "_common.json.gz"), rd(circ + "_vkey.json.gz"))
+        bv = p2v.BatchVerifier(vk, 0, len(cases))
+        res, tr = bv.run(vk.pack_many([rd(c["name"] + "_proof.json.gz") for c in cases]), trace=True)
+        for i, c in enumerate(cases):
+            assert res[i] == c["status"], c["name"]
+            assert [int(x) for x in tr[i]] == [int(x) for x in c["trace"]], c["name"]
+
+
+def test_gpu_n12_standard_batch_vs_oracle(p2v):
+    # BASELINE configs[1] shape (degree_bits 12, 28 queries); distinct proofs at random lanes
+    O = oracle()
+    gc = gen_circuit(12, 4, 0)
+    good = [gc.proof(w, s) for w, s in ((1, 1), (1, 2), (2, 1))]
+
+    def leaf(d):
+        d["proof"]["opening_proof"]["query_round_proofs"][27]["initial_trees_proof"]["evals_proofs"][3][0][0] += 1
+    bad = [mutate(good[0], leaf), gc.proof(2, 5, flags=1)]
+    pool = good + bad
+    expect = [O.verify_json(gc.common, gc.vkey, p) for p in pool]
+    assert expect == [1, 1, 1, -1, -3]
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    packed = vk.pack_many(pool)
+    rng = np.random.default_rng(7)
+    idx = rng.integers(0, len(pool), 300)
+    bv = p2v.BatchVerifier(vk, 0, 300)
+    res, tr = bv.run(packed[idx], trace=True)
+    assert list(res) == [expect[i] for i in idx]
+    for k in range(len(pool)):
+        lanes = np.nonzero(idx == k)[0]
+        if len(lanes):
+            st, otr = O.verify_json(gc.common, gc.vkey, pool[k], trace=True)
+            assert np.array_equal(tr[lanes[0]], otr)
+            assert (tr[lanes] == tr[lanes[0]]).all()
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 257])
+def test_gpu_ragged_batch_sizes(p2v, n):
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    good = vk.pack(gc.proof(1, 1))
+    bad = vk.pack(gc.proof(1, 5, flags=2))
+    arr = np.stack([good if i % 5 else bad for i in range(n)])
+    bv = p2v.BatchVerifier(vk, 0, 300)
+    res = bv.run(arr)
+    assert list(res) == [1 if i % 5 else 0 for i in range(n)]
+
+
+def test_gpu_full_size_properties(p2v):
+    """4096 std-config proofs (BASELINE configs[1] size): every valid proof accepts, a
+    single corrupted lane flips only itself (lane isolation), and re-running the same
+    batch is idempotent."""
+    gc = gen_circuit(12, 4, 0)
+    pool = [gc.proof(w, s) for w, s in ((1, 3), (2, 4))]
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    packed = vk.pack_many(pool)
+    B = 4096
+    arr = np.ascontiguousarray(packed[np.arange(B) % 2])
+    arr[1234, vk.info.proof_words - 7] ^= 1          # a sibling word of the last query's last step
+    bv = p2v.BatchVerifier(vk, 0, B)
+    r1 = bv.run(arr)
+    r2 = bv.run(arr)
+    assert np.array_equal(r1, r2)
+    assert r1[1234] == -2
+    assert (np.delete(r1, 1234) == 1).all()
+
+
+def test_verify_proof_api(p2v):
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    assert p2v.verify_proof(vk, gc.proof(1, 1)) is True
+    assert p2v.verify_proof(vk, gc.proof(1, 5, flags=2)) is False
+    with pytest.raises(p2v.VerifierError) as e:
+        p2v.verify_proof(vk, gc.proof(1, 4, flags=1))
+    assert e.value.status == -3
+    out = p2v.verify_proof_batch(vk, [gc.proof(1, 1), gc.proof(1, 6, flags=4)])
+    assert out == [True, False]

@@ -1,0 +1,132 @@
+"""libp2v host side (no GPU needed): the C-ABI loads and exports every symbol that
+include/p2v.h declares, VerifierCircuitData decoding / validation, proof packing."""
+import ctypes
+import gzip
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+from support import GOLDEN, P, P2V_SO, ROOT, gen_circuit, mutate, p2v_module
+
+
+def test_lib_exports_every_declared_symbol():
+    hdr = open(os.path.join(ROOT, "include", "p2v.h")).read()
+    names = sorted(set(re.findall(r"\b(p2v_[a-z_]+)\s*\(", hdr)))
+    assert len(names) >= 13
+    L = ctypes.CDLL(P2V_SO)
+    for n in names:
+        assert hasattr(L, n), n
+
+
+def test_circuit_info_and_layout():
+    p2v = p2v_module()
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    i = vk.info
+    assert (i.degree_bits, i.lde_bits, i.cap_height, i.num_challenges, i.num_query_rounds) == (6, 9, 4, 2, 28)
+    assert i.oracle_widths == (85, 135, 20, 16)          # commentary/FRI.md:256
+    assert i.step_arity_bits == (4,) and i.final_poly_len == 4
+    assert i.num_openings_this == 5 + 80 + 135 + 2 + 18 + 16 and i.num_openings_next == 2
+    packed = vk.pack(gc.proof(1, 1))
+    assert packed.shape == (i.proof_words,) and packed.dtype == np.uint64
+    assert int(packed.max()) < P
+
+
+def test_std_n12_layout_bytes():
+    # ≈127 KB packed per standard proof at n = 12 (4 public inputs here)
+    p2v = p2v_module()
+    gc = gen_circuit(12, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    assert vk.info.step_arity_bits == (4, 4) and vk.info.final_poly_len == 16
+    assert abs(vk.info.proof_words * 8 - 127016) <= 64
+
+
+def test_pack_canonicalises_and_matches_across_encodings():
+    p2v = p2v_module()
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    pr = gc.proof(2, 3)
+
+    def shift(d):
+        d["public_inputs"][1] += 3 * P
+        d["proof"]["openings"]["constants"][0][0] -= P
+    a, b = vk.pack(pr), vk.pack(mutate(pr, shift))
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("edit,code", [
+    (lambda d: d["proof"]["opening_proof"]["query_round_proofs"].pop(), -3),
+    (lambda d: d["proof"]["openings"]["wires"].pop(), -3),
+    (lambda d: d["proof"]["wires_cap"].pop(), -3),
+    (lambda d: d["proof"]["opening_proof"]["final_poly"]["coeffs"].append([1, 2]), -3),
+    (lambda d: d["proof"].pop("openings"), -1),
+    (lambda d: d["proof"]["openings"].__setitem__("wires", 5), -1),
+])
+def test_pack_shape_and_parse_errors(edit, code):
+    p2v = p2v_module()
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    with pytest.raises(p2v.P2VError) as e:
+        vk.pack(mutate(gc.proof(1, 1), edit))
+    assert e.value.code == code
+    with pytest.raises(p2v.P2VError) as e:
+        vk.pack(b"{not json")
+    assert e.value.code == -1
+
+
+def _common_edit(fn):
+    gc = gen_circuit(6, 4, 0)
+    d = json.loads(gc.common)
+    fn(d)
+    return json.dumps(d).encode(), gc.vkey
+
+
+@pytest.mark.parametrize("edit", [
+    lambda d: d["gates"].__setitem__(0, "MysteryGate { x: 1 }"),                        # Constraints.hs:108
+    lambda d: d["gates"].__setitem__(0, "ExponentiationGate { num_power_bits: 66, y: 1 }"),
+    lambda d: d["config"]["fri_config"].__setitem__("reduction_strategy", {"MinSize": None}),   # Plonk/FRI.hs:342
+    lambda d: d.__setitem__("num_constants", d["num_constants"] + 1),                   # Selector.hs:33-37
+    lambda d: d.__setitem__("num_lookup_selectors", 3),                                 # Selector.hs:31-32
+    lambda d: d["gates"].__setitem__(1, "ArithmeticGate { num_ops: 40 }"),              # reads wire 159 > 134
+    lambda d: d.__setitem__("num_partial_products", 3),                                 # combineInitial sanity
+])
+def test_circuit_level_errors_surface_at_creation(edit):
+    p2v = p2v_module()
+    common, vkey = _common_edit(edit)
+    with pytest.raises(p2v.P2VError) as e:
+        p2v.VerifierCircuitData.from_json(common, vkey)
+    assert e.value.code == -2
+
+
+def test_fixed_reduction_strategy_is_accepted():
+    p2v = p2v_module()
+    common, vkey = _common_edit(lambda d: d["config"]["fri_config"].__setitem__("reduction_strategy", {"Fixed": [3, 1]}))
+    vk = p2v.VerifierCircuitData.from_json(common, vkey)
+    assert vk.info.step_arity_bits == (3, 1)
+
+
+def test_golden_fixtures_pack():
+    p2v = p2v_module()
+    exp = json.load(open(os.path.join(GOLDEN, "expected.json")))["cases"]
+
+    def rd(n):
+        with gzip.open(os.path.join(GOLDEN, n), "rb") as f:
+            return f.read()
+    for case in exp:
+        vk = p2v.VerifierCircuitData.from_json(rd(case["circuit"] + "_common.json.gz"), rd(case["circuit"] + "_vkey.json.gz"))
+        assert vk.pack(rd(case["name"] + "_proof.json.gz")).size == vk.info.proof_words
+        assert vk.info.trace_words == len(case["trace"])
+
+
+def test_verification_fails_loudly_without_gpu():
+    p2v = p2v_module()
+    if p2v.device_count() > 0:
+        pytest.skip("GPU present")
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    with pytest.raises(p2v.P2VError) as e:
+        p2v.verify_proof(vk, gc.proof(1, 1))
+    assert e.value.code == -6   # P2V_E_NODEVICE: no CPU fallback

@@ -1,0 +1,160 @@
+"""Pins the ORACLE (oracle/oracle.c, the CPU restatement of the reference) against the
+reference's own known answers, and checks generator self-consistency (CPU only)."""
+import gzip
+import json
+import os
+
+import numpy as np
+import pytest
+
+from support import GOLDEN, KAT_IN, KAT_OUT, P, gen_circuit, mutate, oracle
+
+
+def test_poseidon_kat():
+    # the reference's only result-pinning vector: Hash/Poseidon.hs:27-35
+    assert oracle().permute(KAT_IN) == KAT_OUT
+
+
+def test_roots_of_unity_sage_identities():
+    # Algebra/Goldilocks.hs:58-67: h = g^((p-1)/2^32) == twoAdicGen; rootsOfUnity!k = h^(2^(32-k))
+    O = oracle().L
+    g, h = 0xc65c18b67785d900, 0x64fdd1a46201e246
+    assert pow(g, (P - 1) // 2**32, P) == h
+    for q in (2, 3, 5, 17, 257, 65537):   # p - 1 = 2^32 * 3 * 5 * 17 * 257 * 65537
+        assert pow(g, (P - 1) // q, P) != 1
+    assert O.or_subgroup_gen(32) == h
+    for k in range(0, 33):
+        w = O.or_subgroup_gen(k)
+        assert w == pow(h, 2 ** (32 - k), P)
+        assert pow(w, 2**k, P) == 1
+        if k > 0:
+            assert pow(w, 2 ** (k - 1), P) != 1
+
+
+def test_field_inverse_semantics():
+    O = oracle().L
+    assert O.or_finv(0) == 0          # inv = pow x (p-2): inv 0 = 0 (Goldilocks.hs:155-156)
+    rng = np.random.default_rng(1)
+    for x in [1, 2, P - 1, P - 2, 2**32 - 1, 2**32] + [int(v) for v in rng.integers(1, 2**63, 50)]:
+        assert O.or_fmul(x % P, O.or_finv(x % P)) == 1
+
+
+@pytest.mark.parametrize("gate,kind", [
+    ("ArithmeticGate { num_ops: 20 }", 0),
+    ("ArithmeticGate { num_ops: 20 } trailing", 16),          # withEOF -> UnknownGate
+    ("ArithmeticExtensionGate { num_ops: 10 }", 1),
+    ("BaseSumGate { num_limbs: 63 } + Base: 2", 2),
+    ("ConstantGate { num_consts: 2 }<anything>", 4),           # no EOF check
+    ("ExponentiationGate { num_power_bits: 66 }", 5),
+    ("ExponentiationGate { num_power_bits: 66, _phantom: PhantomData<x> }<D=2>", 16),
+    ("LookupGate { num_slots: 40, lut_hash: [1, 2, 3] }", 6),
+    ("LookupTableGate { num_slots: 26, lut_hash: [], last_lut_row: 7 }", 7),
+    ("MulExtensionGate { num_ops: 13 }", 8),
+    ("NoopGate", 9),
+    ("PublicInputGate", 10),
+    ("PoseidonGate(PhantomData<plonky2_field::goldilocks_field::GoldilocksField>)<WIDTH=12>", 11),
+    ("PoseidonMdsGate(PhantomData<plonky2_field::goldilocks_field::GoldilocksField>)<WIDTH=12>", 12),
+    ("RandomAccessGate { bits: 4, num_copies: 4, num_extra_constants: 2, _phantom: PhantomData<plonky2_field::goldilocks_field::GoldilocksField> }<D=2>", 13),
+    ("ReducingGate { num_coeffs: 43 }", 14),
+    ("ReducingExtensionGate { num_coeffs: 32 }", 15),
+    ("SomethingElse", 16),
+])
+def test_gate_parser_grammar(gate, kind):
+    # Gate/Parser.hs:112-240
+    assert oracle().L.or_gate_kind(gate.encode()) == kind
+
+
+def test_generated_proofs_accept_and_perm_count():
+    O = oracle()
+    for lk in (0, 1):
+        gc = gen_circuit(6, 4, lk)
+        for w, s in ((1, 1), (2, 3)):
+            O.L.or_perm_count_reset()
+            assert O.verify_json(gc.common, gc.vkey, gc.proof(w, s)) == 1
+    # permutation-count model of SURVEY.md §8d at n = 6 (1727) + ceil(#PI/8) for the PI hash
+    gc = gen_circuit(6, 4, 0)
+    pr = gc.proof(1, 1)
+    c, p = O.circuit(gc.common, gc.vkey), O.proof(pr)
+    O.L.or_perm_count_reset()
+    assert O.verify(c, p) == 1
+    assert O.L.or_perm_count() == 1727 + 1
+
+
+@pytest.mark.slow
+def test_perm_count_matches_commentary_at_n12():
+    # commentary/FRI.md:263-265: 114 + 28 x (77 + 11 + 7) = 2774 permutations (+1: PI hash)
+    O = oracle()
+    gc = gen_circuit(12, 4, 0)
+    c, p = O.circuit(gc.common, gc.vkey), O.proof(gc.proof(1, 1))
+    O.L.or_perm_count_reset()
+    assert O.verify(c, p) == 1
+    assert O.L.or_perm_count() == 2774 + 1
+
+
+def _reject_cases(gc):
+    base = gc.proof(1, 3)
+
+    def leaf(d):
+        d["proof"]["opening_proof"]["query_round_proofs"][3]["initial_trees_proof"]["evals_proofs"][0][0][1] += 1
+
+    def sib(d):
+        d["proof"]["opening_proof"]["query_round_proofs"][2]["steps"][0]["merkle_proof"]["siblings"][0]["elements"][1] += 1
+
+    def powm(d):
+        d["proof"]["opening_proof"]["pow_witness"] += 1
+
+    def wire(d):
+        d["proof"]["openings"]["wires"][3][0] += 1
+
+    def later_leaf_after_final_fail(d):   # round 0 is decided first
+        d["proof"]["opening_proof"]["query_round_proofs"][9]["initial_trees_proof"]["evals_proofs"][1][0][0] += 1
+    return [
+        (gc.proof(1, 4, flags=1), -3),   # step-0 evaluation mismatch  (Plonk/FRI.hs:311)
+        (gc.proof(1, 5, flags=2), 0),    # final polynomial mismatch -> False
+        (gc.proof(1, 6, flags=4), 0),    # Plonk identity fails: FRI never evaluated
+        (mutate(base, leaf), -1),        # initial-tree Merkle failure (Plonk/FRI.hs:108)
+        (mutate(base, sib), -2),         # step Merkle failure (Plonk/FRI.hs:310)
+        (mutate(base, powm), 0),         # proof-of-work (Plonk/FRI.hs:212-216)
+        (mutate(base, wire), 0),         # opening changed: Plonk identity fails
+        (mutate(gc.proof(1, 5, flags=2), later_leaf_after_final_fail), 0),
+    ]
+
+
+@pytest.mark.parametrize("lk", [0, 1])
+def test_reject_paths_follow_reference_order(lk):
+    O = oracle()
+    gc = gen_circuit(6, 4, lk)
+    for proof, expect in _reject_cases(gc):
+        assert O.verify_json(gc.common, gc.vkey, proof) == expect
+
+
+def test_value_canonicalisation_in_json():
+    # aeson Integer then mod p (Goldilocks.hs:98-102): x + p and x - p decode to x
+    O = oracle()
+    gc = gen_circuit(6, 4, 0)
+    pr = gc.proof(2, 3)
+
+    def plus_p(d):
+        d["public_inputs"][0] += P
+        d["proof"]["openings"]["wires"][5][1] -= P
+    assert O.verify_json(gc.common, gc.vkey, mutate(pr, plus_p)) == 1
+
+
+def _golden():
+    with open(os.path.join(GOLDEN, "expected.json")) as f:
+        exp = json.load(f)["cases"]
+
+    def rd(name):
+        with gzip.open(os.path.join(GOLDEN, name), "rb") as f:
+            return f.read()
+    return exp, rd
+
+
+def test_golden_fixtures_oracle():
+    exp, rd = _golden()
+    O = oracle()
+    for case in exp:
+        common, vkey = rd(case["circuit"] + "_common.json.gz"), rd(case["circuit"] + "_vkey.json.gz")
+        st, tr = O.verify_json(common, vkey, rd(case["name"] + "_proof.json.gz"), trace=True)
+        assert st == case["status"], case["name"]
+        assert [int(x) for x in tr] == [int(x) for x in case["trace"]], case["name"]
