@@ -177,11 +177,16 @@ def main():
         kb = kernel_bytes_model(info, info.trace_words)
         dom = max(kavg, key=kavg.get)
         achieved = kb[dom] * B / (kavg[dom] * 1e-3) / 1e9
-        traffic = None
+        # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
+        # (profiles/pmc_traffic.json, corrected per MI355X_MICROARCH.md §HBM), as GB/s over
+        # this run's measured launch time; null if no PMC summary is present.
+        traffic, traffic_bytes = None, None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc):
             try:
-                traffic = json.load(open(pmc)).get(dom)
+                traffic_bytes = json.load(open(pmc)).get(dom)
+                if traffic_bytes:
+                    traffic = round(traffic_bytes / (kavg[dom] * 1e-3) / 1e9, 2)
             except Exception:
                 traffic = None
         ppp = perms_per_proof(info) + 114 + 1
@@ -194,6 +199,7 @@ def main():
                        "global_batch": B * world, "degree_bits": info.degree_bits, "parallelism": f"proof-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
+                         "traffic_bytes_per_launch": traffic_bytes, "algorithmic_bytes_per_launch": kb[dom] * B,
                          "note": "integer-VALU bound (Poseidon); HBM fraction reported as the metric asks"},
             "valu": {"perms_per_proof": ppp, "perm_rate_G": round(value / world * ppp / 1e9, 3)},
             "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
