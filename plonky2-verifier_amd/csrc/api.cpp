@@ -24,6 +24,7 @@ namespace {
 thread_local std::string g_err;
 int fail(int code, const std::string& msg) { g_err = msg; return code; }
 
+// per-kernel timing slots; k_fri and k_vanish run on the side stream concurrently with k_merkle
 const char* kKernelNames = "k_transpose,k_phase1,k_merkle,k_fri,k_vanish,k_status";
 constexpr int kNumKernels = 6;
 
@@ -57,7 +58,9 @@ struct p2v_verifier {
   std::vector<DevBuf> bufs;
   DevBuf in, soa, chal, leafdig, mk, fbits, qvals, van, res, trace;
   DevBuf t_cs, t_kis, t_gkind, t_gpar, t_ggrp, t_gwoff, t_w, t_gs, t_ge, t_lin, t_lout, t_loff, t_llen, t_tw, t_ops;
-  hipEvent_t ev[kNumKernels + 1];
+  hipEvent_t ev[2 * kNumKernels];   // start/end per kernel
+  hipEvent_t dep_p1 = nullptr, dep_side = nullptr;
+  hipStream_t side = nullptr;
   float last_ms[kNumKernels] = {0};
   bool timed = false;
 };
@@ -125,6 +128,9 @@ void p2v_verifier_free(p2v_verifier* v) {
                     &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops})
     b->free_();
   if (v->timed) for (auto& e : v->ev) (void)hipEventDestroy(e);
+  if (v->dep_p1) (void)hipEventDestroy(v->dep_p1);
+  if (v->dep_side) (void)hipEventDestroy(v->dep_side);
+  if (v->side) (void)hipStreamDestroy(v->side);
   delete v;
 }
 
@@ -188,7 +194,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   {
     const int r = d.r, C4 = 4 * C.cap_len;
     op(TOP_ABSORB_DIGEST, 0, 4);
-    op(TOP_ABSORB_CHAL, CH_PI(d), 4);
+    op(TOP_ABSORB_PIH, 0, 4);
     op(TOP_ABSORB_SOA, L.wcap, C4);
     op(TOP_SQUEEZE, CH_BETA(d), r);
     op(TOP_SQUEEZE, CH_GAMMA(d), r);
@@ -225,6 +231,9 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (e == hipSuccess) e = v->res.alloc(B);
   if (e == hipSuccess) e = v->trace.alloc((size_t)C.trace_words * B * 8);
   if (e == hipSuccess) { for (auto& x : v->ev) { e = hipEventCreate(&x); if (e != hipSuccess) break; } v->timed = e == hipSuccess; }
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_p1, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_side, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&v->side, hipStreamNonBlocking);
   if (e != hipSuccess) { p2v_verifier_free(v); return fail(P2V_E_DEVICE, std::string("device allocation: ") + hipGetErrorString(e)); }
   d.cs_cap = (const uint64_t*)v->t_cs.p; d.k_is = (const uint64_t*)v->t_kis.p; d.gate_kind = (const int32_t*)v->t_gkind.p;
   d.gate_par = (const int64_t*)v->t_gpar.p; d.gate_grp = (const int32_t*)v->t_ggrp.p; d.gate_woff = (const int32_t*)v->t_gwoff.p;
@@ -258,21 +267,39 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   if (trace) dtrace = (flags & P2V_FLAG_RESULT_DEVICE) ? trace : (uint64_t*)v->trace.p;
   const int NPB = d.B / 64;
   const bool tm = v->timed;
-  if (tm) HCK(hipEventRecord(v->ev[0], st));
+  hipStream_t sd = v->side;
+#define T0(k, s_) do { if (tm) HCK(hipEventRecord(v->ev[2 * (k)], s_)); } while (0)
+#define T1(k, s_) do { if (tm) HCK(hipEventRecord(v->ev[2 * (k) + 1], s_)); } while (0)
+  T0(0, st);
   k_transpose<<<dim3((unsigned)((words + 63) / 64), NPB), 256, 0, st>>>(src, words, (int)n, (uint64_t*)v->soa.p, d.B);
-  if (tm) HCK(hipEventRecord(v->ev[1], st));
-  const int nt_blocks = (d.B + 255) / 256;
+  T1(0, st);
+  // phase 1: transcript waves + leaf-hash waves in one launch (the leaf sponges do not
+  // depend on the challenges, so they fill the GPU while the serial transcripts run)
+  const int nt_blocks = (4 * d.B + 255) / 256;   // 4 lanes per proof
   const int leaf_units = d.Q * d.T * NPB;
+  T0(1, st);
   k_phase1<<<nt_blocks + (leaf_units + 3) / 4, 256, 0, st>>>(d, nt_blocks);
-  if (tm) HCK(hipEventRecord(v->ev[2], st));
+  T1(1, st);
+  // phase 2: Merkle paths on the main stream; FRI queries and the vanishing kernel (few,
+  // long-latency waves) on the side stream, concurrently
+  HCK(hipEventRecord(v->dep_p1, st));
+  HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));
+  T0(4, sd);
+  k_vanish<<<(d.B + 255) / 256, 256, 0, sd>>>(d);
+  T1(4, sd);
+  T0(3, sd);
+  k_fri<<<(d.Q * NPB + 3) / 4, 256, 0, sd>>>(d);
+  T1(3, sd);
+  HCK(hipEventRecord(v->dep_side, sd));
+  T0(2, st);
   k_merkle<<<(leaf_units + 3) / 4, 256, 0, st>>>(d);
-  if (tm) HCK(hipEventRecord(v->ev[3], st));
-  k_fri<<<(d.Q * NPB + 3) / 4, 256, 0, st>>>(d);
-  if (tm) HCK(hipEventRecord(v->ev[4], st));
-  k_vanish<<<(d.B + 255) / 256, 256, 0, st>>>(d);
-  if (tm) HCK(hipEventRecord(v->ev[5], st));
+  T1(2, st);
+  HCK(hipStreamWaitEvent(st, v->dep_side, 0));
+  T0(5, st);
   k_status<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(d, dres, dtrace, C.trace_words);
-  if (tm) HCK(hipEventRecord(v->ev[6], st));
+  T1(5, st);
+#undef T0
+#undef T1
   HCK(hipGetLastError());
   if (!(flags & P2V_FLAG_RESULT_DEVICE)) {
     HCK(hipMemcpyAsync(results, dres, n, hipMemcpyDeviceToHost, st));
@@ -280,7 +307,7 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   }
   if (!(flags & P2V_FLAG_NO_SYNC) || !(flags & P2V_FLAG_RESULT_DEVICE)) {
     HCK(hipStreamSynchronize(st));
-    if (tm) for (int k = 0; k < kNumKernels; k++) { float ms = 0; if (hipEventElapsedTime(&ms, v->ev[k], v->ev[k + 1]) == hipSuccess) v->last_ms[k] = ms; }
+    if (tm) for (int k = 0; k < kNumKernels; k++) { float ms = 0; if (hipEventElapsedTime(&ms, v->ev[2 * k], v->ev[2 * k + 1]) == hipSuccess) v->last_ms[k] = ms; }
   }
   return P2V_OK;
 }

@@ -59,7 +59,7 @@ struct DevCircuit {
 
 // transcript op program (built on the host from the circuit; uniform across the batch)
 #define TOP_ABSORB_SOA 0    // absorb n words of the proof (SoA) from word a
-#define TOP_ABSORB_CHAL 1   // absorb n words of the challenge buffer from word a
+#define TOP_ABSORB_PIH 1    // absorb the 4-word public-inputs hash
 #define TOP_ABSORB_DIGEST 2 // absorb the circuit digest (n = 4)
 #define TOP_SQUEEZE 3       // squeeze n words into challenge words a..
 #define TOP_SQUEEZE_IDX 4   // squeeze n query indices (mod 2^lde_bits) into a..

@@ -17,6 +17,7 @@
 //                 (proof, query)  (Plonk/FRI.hs:151-407)
 //   k_status      reference evaluation order -> int8 status (+ optional trace)
 #include "devcommon.h"
+#include "qposeidon.h"
 
 using namespace p2d;
 using gl::E;
@@ -65,79 +66,102 @@ __device__ __forceinline__ void leaf_hash_unit(const DevCircuit& c, int unit, in
 
 // The transcript (Challenge/Verifier.hs:58-103, Challenge/FRI.hs:65-104) is a fixed
 // sequence of absorbs and squeezes for a given circuit; the host compiles it into an op
-// program and this loop interprets it with ONE permutation call site (the code size of
-// an inlined permutation is ~3k instructions).
-__device__ __forceinline__ void transcript_lane(const DevCircuit& c, int p) {
+// program and this loop interprets it with ONE permutation call site.  Each proof's
+// duplex state is spread over a lane quad (qposeidon.h): the ~114 permutations form a
+// strictly serial chain, so per-permutation latency, not throughput, is what counts.
+__device__ __forceinline__ void transcript_quad(const DevCircuit& c, int p, int t) {
   // public inputs hash, Hash/Sponge.hs:26-31 (sponge [] = zero digest)
-  {
-    uint64_t st[12];
-#pragma unroll
-    for (int i = 0; i < 12; i++) st[i] = 0;
-    for (int i = 0; i < c.num_pis; i += 8) {
-      const int k = c.num_pis - i;
-#pragma unroll
-      for (int j = 0; j < 8; j++) if (j < k) st[j] = ld(c, c.pis + i + j, p);
-      p2::permute(st);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++) chal(c, CH_PI(c) + i, p) = st[i];
+  uint64_t x[3] = {0, 0, 0};
+  for (int i = 0; i < c.num_pis; i += 8) {
+    const int k = c.num_pis - i;
+    for (int j = 0; j < 8 && j < k; j++) qp::set_word(x, t, j, ld(c, c.pis + i + j, p));
+    qp::permute(x, t);
   }
-  uint64_t s[12];
+  uint64_t pih[4];
 #pragma unroll
-  for (int i = 0; i < 12; i++) s[i] = 0;
+  for (int w = 0; w < 4; w++) {
+    pih[w] = qp::get_word(x, w);
+    if (t == 0) chal(c, CH_PI(c) + w, p) = pih[w];
+  }
+  x[0] = x[1] = x[2] = 0;
   int nbuf = 0, outpos = -1;
   bool absorbing = true;
   const uint64_t qmask = (1ULL << c.lde_bits) - 1;
+  uint64_t fa0 = 0, fa1 = 0;   // FRI alpha, kept in registers for the reduced openings below
   for (int o = 0; o < c.ntops; o++) {
     const int type = c.tops[3 * o], a = c.tops[3 * o + 1], n = c.tops[3 * o + 2];
     if (type == TOP_COPY) {   // mkLookupDeltaList (betas ++ gammas ++ ...), Challenge/Verifier.hs:36-40,82-86
-      for (int k = 0; k < n; k++) chal(c, a + k, p) = chal(c, a - 3 * c.r + k, p);
+      if (t == 0) for (int k = 0; k < n; k++) chal(c, a + k, p) = chal(c, a - 3 * c.r + k, p);
       continue;
     }
     if (type == TOP_ZERO) {
-      for (int k = 0; k < n; k++) chal(c, a + k, p) = 0;
+      if (t == 0) for (int k = 0; k < n; k++) chal(c, a + k, p) = 0;
       continue;
     }
     const bool ab = type <= TOP_ABSORB_DIGEST;
     for (int k = 0; k < n; k++) {
-      uint64_t x = 0;
-      if (type == TOP_ABSORB_SOA) x = ld(c, (int64_t)a + k, p);
-      else if (type == TOP_ABSORB_CHAL) x = chal(c, a + k, p);
-      else if (type == TOP_ABSORB_DIGEST) x = c.digest[k & 3];
+      uint64_t v = 0;
+      if (type == TOP_ABSORB_SOA) v = ld(c, (int64_t)a + k, p);
+      else if (type == TOP_ABSORB_PIH) v = pih[k & 3];
+      else if (type == TOP_ABSORB_DIGEST) v = c.digest[k & 3];
       bool need;
       if (ab) { if (!absorbing) { absorbing = true; nbuf = 0; } need = nbuf == 8; }
       else need = absorbing || outpos < 0;
-      if (need) p2::permute(s);   // duplex / re-permute, Challenge/Pure.hs:38-69
+      if (need) qp::permute(x, t);   // duplex / re-permute, Challenge/Pure.hs:38-69
       if (ab) {
         if (need) nbuf = 0;
-        st_set(s, nbuf, x);   // overwrite mode: input lands in the rate part
+        qp::set_word(x, t, nbuf, v);   // overwrite mode: input lands in the rate part
         nbuf++;
       } else {
         if (need) { absorbing = false; outpos = 7; }
-        uint64_t v = st_get(s, outpos);   // output order state[7], state[6], ... (reverse of take 8)
+        uint64_t w = qp::get_word(x, outpos);   // output order state[7], state[6], ... (reverse of take 8)
         outpos--;
-        if (type == TOP_SQUEEZE_IDX) v &= qmask;
-        chal(c, a + k, p) = v;
+        if (type == TOP_SQUEEZE_IDX) w &= qmask;
+        if (a + k == CH_FRI_ALPHA(c)) fa0 = w;
+        if (a + k == CH_FRI_ALPHA(c) + 1) fa1 = w;
+        if (t == 0) chal(c, a + k, p) = w;
       }
     }
   }
-  // precomputeReducedOpenings, Plonk/FRI.hs:128-134: Y = sum alpha^i y_i (Horner from the end)
-  const E alpha = chal_e(c, CH_FRI_ALPHA(c), p);
-  E y0 = gl::e0(), y1 = gl::e0();
-  for (int64_t i = c.n_this - 1; i >= 0; i--) y0 = gl::eadd(gl::emul(y0, alpha), lde(c, c.o_const + 2 * i, p));
-  for (int64_t i = c.n_next - 1; i >= 0; i--) y1 = gl::eadd(gl::emul(y1, alpha), lde(c, c.o_zs_next + 2 * i, p));
-  chal(c, CH_Y0(c), p) = y0.a; chal(c, CH_Y0(c) + 1, p) = y0.b;
-  chal(c, CH_Y1(c), p) = y1.a; chal(c, CH_Y1(c) + 1, p) = y1.b;
+  // precomputeReducedOpenings, Plonk/FRI.hs:128-134: Y = sum alpha^i y_i.  Split over the
+  // quad: lane t sums the terms i = t (mod 4) in powers of alpha^4, then Y = sum_t alpha^t H_t.
+  const E alpha{fa0, fa1};
+  const E al2 = gl::emul(alpha, alpha), al4 = gl::emul(al2, al2);
+  E H[2];
+#pragma unroll
+  for (int b = 0; b < 2; b++) {
+    const int64_t n = b == 0 ? c.n_this : c.n_next, off = b == 0 ? c.o_const : c.o_zs_next;
+    const int64_t M = (n + 3) / 4;
+    E h = gl::e0();
+    for (int64_t m = M - 1; m >= 0; m--) {
+      const int64_t i = 4 * m + t;
+      const E y = i < n ? lde(c, off + 2 * i, p) : gl::e0();
+      h = gl::eadd(gl::emul(h, al4), y);
+    }
+    H[b] = h;
+  }
+#pragma unroll
+  for (int b = 0; b < 2; b++) {
+    E h1{qp::bcast64(H[b].a, 1), qp::bcast64(H[b].b, 1)};
+    E h2{qp::bcast64(H[b].a, 2), qp::bcast64(H[b].b, 2)};
+    E h3{qp::bcast64(H[b].a, 3), qp::bcast64(H[b].b, 3)};
+    E h0{qp::bcast64(H[b].a, 0), qp::bcast64(H[b].b, 0)};
+    const E y = gl::eadd(h0, gl::emul(alpha, gl::eadd(h1, gl::emul(alpha, gl::eadd(h2, gl::emul(alpha, h3))))));
+    if (t == 0) { chal(c, (b == 0 ? CH_Y0(c) : CH_Y1(c)), p) = y.a; chal(c, (b == 0 ? CH_Y0(c) : CH_Y1(c)) + 1, p) = y.b; }
+  }
 }
 
 // ------------------------------------------------------------------------ phase 1
-// blocks [0, nt_blocks): transcript (4 waves x 64 proofs); the rest: leaf hashing, 4 units
-// per block.  Transcript blocks come first so their long serial chains start early.
+// blocks [0, nt_blocks): transcript quads (64 proofs per block, 4 lanes each, at raised
+// wave priority so co-resident leaf waves do not stretch the serial chain); the rest:
+// leaf hashing, 4 units per block.  Transcript blocks come first so they start first.
 extern "C" __global__ void __launch_bounds__(256) k_phase1(DevCircuit c, int nt_blocks) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if ((int)blockIdx.x < nt_blocks) {
-    const int p = blockIdx.x * 256 + threadIdx.x;
-    if (p < c.B) transcript_lane(c, p);
+    __builtin_amdgcn_s_setprio(3);
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    const int p = g >> 2, t = g & 3;
+    if (p < c.B) transcript_quad(c, p, t);
     return;
   }
   const int unit = ((int)blockIdx.x - nt_blocks) * 4 + wave;

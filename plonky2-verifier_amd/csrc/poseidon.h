@@ -30,12 +30,24 @@ static __constant__ uint64_t c_fast_init_matrix[11 * 11] = P2V_FAST_PARTIAL_ROUN
 #endif
 static const uint64_t h_round_constants[360] = P2V_ALL_ROUND_CONSTANTS_INIT;
 
+// Inside the permutation values are kept in [0, 2^64) (congruent mod p, not necessarily
+// canonical); the 12 outputs are canonicalised once at the end.  This removes the
+// compare/select of every add and multiply (~13% of the instruction stream).
+__host__ __device__ __forceinline__ uint64_t add_nc(uint64_t a, uint64_t b) {   // a < 2^64, b < p
+  uint64_t s = a + b;
+  return s + ((s < a) ? gl::EPS : 0);   // a + b - 2^64 + EPS < 2^64: no second carry
+}
+__host__ __device__ __forceinline__ uint64_t mul_nc(uint64_t a, uint64_t b) {
+  uint64_t hi, lo;
+  gl::mul128(a, b, hi, lo);
+  return gl::reduce128_nc(hi, lo);
+}
 // x^7
 __host__ __device__ __forceinline__ uint64_t sbox(uint64_t x) {
-  uint64_t x2 = gl::mul(x, x);
-  uint64_t x3 = gl::mul(x, x2);
-  uint64_t x4 = gl::mul(x2, x2);
-  return gl::mul(x3, x4);
+  uint64_t x2 = mul_nc(x, x);
+  uint64_t x3 = mul_nc(x, x2);
+  uint64_t x4 = mul_nc(x2, x2);
+  return mul_nc(x3, x4);
 }
 
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__clang__)
@@ -44,7 +56,8 @@ __host__ __device__ __forceinline__ uint64_t sbox(uint64_t x) {
 #define P2_UNROLL _Pragma("GCC unroll 12")
 #endif
 
-// y = M x with M = circ + diag; inputs canonical, outputs canonical.
+// y = M x with M = circ + diag; inputs any value < 2^64, outputs < 2^64 (lazy).
+// Each row is sum_j c_j x_j with c_j < 2^6, accumulated separately over the 32-bit halves.
 __host__ __device__ __forceinline__ void mds(uint64_t s[12]) {
   uint64_t out[12];
   P2_UNROLL
@@ -59,7 +72,7 @@ __host__ __device__ __forceinline__ void mds(uint64_t s[12]) {
     // value = ah * 2^32 + al,  al, ah < 2^42
     uint64_t l = al + (ah << 32);
     uint64_t h = (ah >> 32) + (l < al ? 1 : 0);
-    out[i] = gl::canon(gl::reduce96_nc(h, l));
+    out[i] = gl::reduce96_nc(h, l);
   }
   P2_UNROLL
   for (int i = 0; i < 12; i++) s[i] = out[i];
@@ -75,17 +88,17 @@ __host__ __device__ __forceinline__ uint64_t round_constant(int idx) {
 
 __host__ __device__ __forceinline__ void full_round(uint64_t s[12], int r) {
   P2_UNROLL
-  for (int i = 0; i < 12; i++) s[i] = sbox(gl::add(s[i], round_constant(12 * r + i)));
+  for (int i = 0; i < 12; i++) s[i] = sbox(add_nc(s[i], round_constant(12 * r + i)));
   mds(s);
 }
 __host__ __device__ __forceinline__ void partial_round(uint64_t s[12], int r) {
-  s[0] = sbox(gl::add(s[0], round_constant(12 * r)));
+  s[0] = sbox(add_nc(s[0], round_constant(12 * r)));
   P2_UNROLL
-  for (int i = 1; i < 12; i++) s[i] = gl::add(s[i], round_constant(12 * r + i));
+  for (int i = 1; i < 12; i++) s[i] = add_nc(s[i], round_constant(12 * r + i));
   mds(s);
 }
 
-// Hash/Poseidon.hs:42-46
+// Hash/Poseidon.hs:42-46.  Inputs may be any value < 2^64; outputs are canonical.
 __host__ __device__ __forceinline__ void permute(uint64_t s[12]) {
 #pragma unroll 1
   for (int r = 0; r < 4; r++) full_round(s, r);
@@ -93,6 +106,8 @@ __host__ __device__ __forceinline__ void permute(uint64_t s[12]) {
   for (int r = 4; r < 26; r++) partial_round(s, r);
 #pragma unroll 1
   for (int r = 26; r < 30; r++) full_round(s, r);
+  P2_UNROLL
+  for (int i = 0; i < 12; i++) s[i] = gl::canon(s[i]);
 }
 
 }  // namespace p2

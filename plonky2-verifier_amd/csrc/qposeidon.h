@@ -1,0 +1,115 @@
+// qposeidon.h — Poseidon-12 spread over a lane QUAD (device only).
+//
+// Used where the permutation is on a serial critical path (the Fiat–Shamir transcript,
+// ~114 dependent permutations per proof, Challenge/Pure.hs): lane t = lane & 3 of the
+// quad owns state words 3t, 3t+1, 3t+2.  Full rounds run three S-boxes per lane instead of
+// twelve; the MDS row i = 3t + m needs every word: the other lanes' words are fetched with
+// DPP quad_perm rotations (lane t reads lane (t+d) & 3), which makes the circulant
+// coefficient of every term wave-uniform: M(3t+m, 3((t+d)&3)+k) = circ[(3d + k - m) mod 12]
+// (+8 on the diagonal entry (0,0), Hash/Constants.hs:21-25).  ~3.6x lower latency per
+// permutation than one lane holding all 12 words.
+#pragma once
+#include "gl.h"
+#include "poseidon.h"
+
+namespace qp {
+
+// quad_perm rotation: lane t reads lane (t + D) & 3
+template <int D>
+__device__ __forceinline__ uint32_t rot32(uint32_t v) {
+  constexpr int ctrl = ((0 + D) & 3) | (((1 + D) & 3) << 2) | (((2 + D) & 3) << 4) | (((3 + D) & 3) << 6);
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, 0xf, 0xf, false);
+}
+template <int D>
+__device__ __forceinline__ uint64_t rot64(uint64_t v) {
+  return ((uint64_t)rot32<D>((uint32_t)(v >> 32)) << 32) | rot32<D>((uint32_t)v);
+}
+// broadcast lane `src` (uniform, 0..3) of each quad
+__device__ __forceinline__ uint32_t bcast32(uint32_t v, int src) {
+  switch (src) {
+    case 0: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x00, 0xf, 0xf, false);
+    case 1: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x55, 0xf, 0xf, false);
+    case 2: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xAA, 0xf, 0xf, false);
+    default: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xFF, 0xf, 0xf, false);
+  }
+}
+__device__ __forceinline__ uint64_t bcast64(uint64_t v, int src) {
+  return ((uint64_t)bcast32((uint32_t)(v >> 32), src) << 32) | bcast32((uint32_t)v, src);
+}
+
+// this lane's round constant for word 3t+k of round r: scalar loads + lane selects
+__device__ __forceinline__ void lane_rc(int r, int t, uint64_t rc[3]) {
+  const uint64_t* R = p2::c_round_constants + 12 * r;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const uint64_t a = R[k], b = R[3 + k], c = R[6 + k], d = R[9 + k];
+    rc[k] = t == 0 ? a : t == 1 ? b : t == 2 ? c : d;
+  }
+}
+
+__device__ __forceinline__ void mds(uint64_t x[3], int t) {
+  uint64_t X[4][3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) { X[0][k] = x[k]; X[1][k] = rot64<1>(x[k]); X[2][k] = rot64<2>(x[k]); X[3][k] = rot64<3>(x[k]); }
+  const uint64_t c00 = t == 0 ? 25 : 17;   // circ[0] (+ diag[0] on row 0)
+  uint64_t out[3];
+#pragma unroll
+  for (int m = 0; m < 3; m++) {
+    uint64_t al = 0, ah = 0;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const int idx = ((3 * d + k - m) % 12 + 12) % 12;
+        const uint64_t c = (m == 0 && d == 0 && k == 0) ? c00 : (uint64_t)p2::MDS_CIRC[idx];
+        al += (uint64_t)(uint32_t)X[d][k] * c;
+        ah += (X[d][k] >> 32) * c;
+      }
+    }
+    uint64_t l = al + (ah << 32);
+    uint64_t h = (ah >> 32) + (l < al ? 1 : 0);
+    out[m] = gl::reduce96_nc(h, l);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; k++) x[k] = out[k];
+}
+
+// the quad's permutation; x = this lane's three words (inputs < 2^64, outputs canonical)
+__device__ __forceinline__ void permute(uint64_t x[3], int t) {
+  uint64_t rc[3];
+#pragma unroll 1
+  for (int r = 0; r < 30; r++) {
+    lane_rc(r, t, rc);
+    const bool full = r < 4 || r >= 26;
+    if (full) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) x[k] = p2::sbox(p2::add_nc(x[k], rc[k]));
+    } else {
+      const uint64_t a = p2::add_nc(x[0], rc[0]);
+      const uint64_t s = p2::sbox(a);   // computed by every lane, kept by lane 0 (word 0)
+      x[0] = t == 0 ? s : a;
+      x[1] = p2::add_nc(x[1], rc[1]);
+      x[2] = p2::add_nc(x[2], rc[2]);
+    }
+    mds(x, t);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; k++) x[k] = gl::canon(x[k]);
+}
+
+// word `pos` (uniform, 0..11) of the quad's state, broadcast to all four lanes
+__device__ __forceinline__ uint64_t get_word(const uint64_t x[3], int pos) {
+  const int k = pos % 3;
+  const uint64_t v = k == 0 ? x[0] : (k == 1 ? x[1] : x[2]);
+  return bcast64(v, pos / 3);
+}
+// write word `pos` (uniform) of the quad's state
+__device__ __forceinline__ void set_word(uint64_t x[3], int t, int pos, uint64_t v) {
+  const int owner = pos / 3, k = pos % 3;
+  const bool mine = t == owner;
+  if (k == 0) x[0] = mine ? v : x[0];
+  else if (k == 1) x[1] = mine ? v : x[1];
+  else x[2] = mine ? v : x[2];
+}
+
+}  // namespace qp
