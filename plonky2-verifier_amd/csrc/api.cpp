@@ -16,6 +16,7 @@ extern "C" __global__ void k_phase1(DevCircuit, int);
 extern "C" __global__ void k_merkle(DevCircuit);
 extern "C" __global__ void k_fri(DevCircuit);
 extern "C" __global__ void k_vanish(DevCircuit);
+extern "C" __global__ void k_vanish_final(DevCircuit);
 extern "C" __global__ void k_status(DevCircuit, int8_t*, uint64_t*, int64_t);
 
 using namespace p2v;
@@ -25,8 +26,8 @@ thread_local std::string g_err;
 int fail(int code, const std::string& msg) { g_err = msg; return code; }
 
 // per-kernel timing slots; k_fri and k_vanish run on the side stream concurrently with k_merkle
-const char* kKernelNames = "k_transpose,k_phase1,k_merkle,k_fri,k_vanish,k_status";
-constexpr int kNumKernels = 6;
+const char* kKernelNames = "k_transpose,k_phase1,k_merkle,k_fri,k_vanish,k_status,k_vanish_final";
+constexpr int kNumKernels = 7;
 
 struct DevBuf {
   void* p = nullptr;
@@ -56,8 +57,8 @@ struct p2v_verifier {
   size_t max_batch = 0, Bmax = 0;
   DevCircuit dc{};
   std::vector<DevBuf> bufs;
-  DevBuf in, soa, chal, leafdig, mk, fbits, qvals, van, res, trace;
-  DevBuf t_cs, t_kis, t_gkind, t_gpar, t_ggrp, t_gwoff, t_w, t_gs, t_ge, t_lin, t_lout, t_loff, t_llen, t_tw, t_ops;
+  DevBuf in, soa, chal, leafdig, mk, fbits, qvals, van, vparts, res, trace;
+  DevBuf t_cs, t_kis, t_gkind, t_gpar, t_ggrp, t_gwoff, t_w, t_gs, t_ge, t_lin, t_lout, t_loff, t_llen, t_tw, t_ops, t_vit;
   hipEvent_t ev[2 * kNumKernels];   // start/end per kernel
   hipEvent_t dep_p1 = nullptr, dep_side = nullptr;
   hipStream_t side = nullptr;
@@ -124,8 +125,8 @@ int p2v_device_count(void) {
 void p2v_verifier_free(p2v_verifier* v) {
   if (!v) return;
   (void)hipSetDevice(v->device);
-  for (DevBuf* b : {&v->in, &v->soa, &v->chal, &v->leafdig, &v->mk, &v->fbits, &v->qvals, &v->van, &v->res, &v->trace, &v->t_cs, &v->t_kis,
-                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops})
+  for (DevBuf* b : {&v->in, &v->soa, &v->chal, &v->leafdig, &v->mk, &v->fbits, &v->qvals, &v->van, &v->vparts, &v->res, &v->trace, &v->t_cs, &v->t_kis,
+                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit})
     b->free_();
   if (v->timed) for (auto& e : v->ev) (void)hipEventDestroy(e);
   if (v->dep_p1) (void)hipEventDestroy(v->dep_p1);
@@ -213,10 +214,24 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
     op(TOP_SQUEEZE_IDX, CH_QIDX(d), d.Q);
   }
   d.ntops = (int)(ops.size() / 3);
+  // vanishing work items, heaviest first so their waves are dispatched first
+  std::vector<int32_t> vit;
+  {
+    auto item = [&](int t, int a_, int b_, int64_t first) { vit.push_back(t); vit.push_back(a_); vit.push_back(b_); vit.push_back((int32_t)first); };
+    for (int g = 0; g < C.n_gate_eval; g++)
+      if (gkind[g] == G_POSEIDON) for (int k = 0; k < P2V_POSEIDON_PARTS; k++) item(VI_GATE, g, k, p2v_poseidon_part_first_term(k));
+    for (int g = 0; g < C.n_gate_eval; g++) if (gkind[g] == G_COSET) item(VI_GATE, g, 0, 0);
+    for (int g = 0; g < C.n_gate_eval; g++) if (gkind[g] != G_POSEIDON && gkind[g] != G_COSET) item(VI_GATE, g, 0, 0);
+    for (int j = 0; j < d.r; j++) item(VI_PP, j, 0, d.r + (int64_t)j * d.n_pp_terms);
+    if (d.nluts > 0)
+      for (int j = 0; j < d.r; j++) item(VI_LOOKUP, j, 0, d.r + (int64_t)d.r * d.n_pp_terms + (int64_t)j * d.n_lookup_terms);
+    item(VI_ZS1, 0, 0, 0);
+  }
+  d.n_vitems = (int)(vit.size() / 4);
   hipError_t e = hipSuccess;
 #define UP(buf, vec) if (e == hipSuccess) e = upload(buf, vec)
   UP(v->t_cs, C.cs_cap); UP(v->t_kis, C.k_is); UP(v->t_gkind, gkind); UP(v->t_gpar, gpar); UP(v->t_ggrp, ggrp); UP(v->t_gwoff, gwoff);
-  UP(v->t_w, wts); UP(v->t_gs, gs); UP(v->t_ge, ge); UP(v->t_lin, lin); UP(v->t_lout, lout); UP(v->t_loff, loff); UP(v->t_llen, llen); UP(v->t_tw, tw); UP(v->t_ops, ops);
+  UP(v->t_w, wts); UP(v->t_gs, gs); UP(v->t_ge, ge); UP(v->t_lin, lin); UP(v->t_lout, lout); UP(v->t_loff, loff); UP(v->t_llen, llen); UP(v->t_tw, tw); UP(v->t_ops, ops); UP(v->t_vit, vit);
 #undef UP
   const size_t B = v->Bmax;
   const size_t chw = (size_t)(4 + 7 * d.r + 4 + 2 * d.S + 1 + d.Q + 4);
@@ -228,6 +243,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (e == hipSuccess) e = v->fbits.alloc((size_t)d.Q * B * 4);
   if (e == hipSuccess) e = v->qvals.alloc((size_t)d.Q * 6 * B * 8);
   if (e == hipSuccess) e = v->van.alloc((size_t)(1 + 4 * d.r) * B * 8);
+  if (e == hipSuccess) e = v->vparts.alloc((size_t)d.n_vitems * 2 * d.r * B * 8);
   if (e == hipSuccess) e = v->res.alloc(B);
   if (e == hipSuccess) e = v->trace.alloc((size_t)C.trace_words * B * 8);
   if (e == hipSuccess) { for (auto& x : v->ev) { e = hipEventCreate(&x); if (e != hipSuccess) break; } v->timed = e == hipSuccess; }
@@ -239,9 +255,9 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   d.gate_par = (const int64_t*)v->t_gpar.p; d.gate_grp = (const int32_t*)v->t_ggrp.p; d.gate_woff = (const int32_t*)v->t_gwoff.p;
   d.weights = (const uint64_t*)v->t_w.p; d.grp_start = (const int32_t*)v->t_gs.p; d.grp_end = (const int32_t*)v->t_ge.p;
   d.lut_in = (const uint64_t*)v->t_lin.p; d.lut_out = (const uint64_t*)v->t_lout.p; d.lut_off = (const int64_t*)v->t_loff.p; d.lut_len = (const int64_t*)v->t_llen.p;
-  d.twiddles = (const uint64_t*)v->t_tw.p; d.tops = (const int32_t*)v->t_ops.p;
+  d.twiddles = (const uint64_t*)v->t_tw.p; d.tops = (const int32_t*)v->t_ops.p; d.vitems = (const int32_t*)v->t_vit.p;
   d.soa = (const uint64_t*)v->soa.p; d.chal = (uint64_t*)v->chal.p; d.leafdig = (uint64_t*)v->leafdig.p; d.mk_ok = (uint8_t*)v->mk.p;
-  d.fri_bits = (uint32_t*)v->fbits.p; d.qvals = (uint64_t*)v->qvals.p; d.van = (uint64_t*)v->van.p;
+  d.fri_bits = (uint32_t*)v->fbits.p; d.qvals = (uint64_t*)v->qvals.p; d.van = (uint64_t*)v->van.p; d.vparts = (uint64_t*)v->vparts.p;
   *out = v;
   return P2V_OK;
 }
@@ -285,8 +301,11 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   HCK(hipEventRecord(v->dep_p1, st));
   HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));
   T0(4, sd);
-  k_vanish<<<(d.B + 255) / 256, 256, 0, sd>>>(d);
+  k_vanish<<<(d.n_vitems * NPB + 3) / 4, 256, 0, sd>>>(d);
   T1(4, sd);
+  T0(6, sd);
+  k_vanish_final<<<(d.B + 255) / 256, 256, 0, sd>>>(d);
+  T1(6, sd);
   T0(3, sd);
   k_fri<<<(d.Q * NPB + 3) / 4, 256, 0, sd>>>(d);
   T1(3, sd);

@@ -47,6 +47,8 @@ struct DevCircuit {
   const uint64_t* twiddles;        // per step: omega_{a}^{-j}, j < 2^a  (offset 256*s)
   const int32_t* tops;             // transcript op program [ntops][3] (see TOP_*)
   int32_t ntops;
+  const int32_t* vitems;           // vanishing work items [n_vitems][4] = {VI_*, a, b, first term}
+  int32_t n_vitems;
   // batch buffers
   const uint64_t* soa;             // [words][B]
   uint64_t* chal;                  // [CH_WORDS][B]
@@ -55,6 +57,7 @@ struct DevCircuit {
   uint32_t* fri_bits;              // [Q][B]: bit s = step-s evaluation check, bit 31 = final check
   uint64_t* qvals;                 // [Q][6][B]: initial, folded, final (F^2 each)
   uint64_t* van;                   // [1 + 4r][B]: eqs_ok, C_i, quotient_i
+  uint64_t* vparts;                // [n_vitems][2r][B]: per-item partial alpha-sums
 };
 
 // transcript op program (built on the host from the circuit; uniform across the batch)
@@ -65,6 +68,18 @@ struct DevCircuit {
 #define TOP_SQUEEZE_IDX 4   // squeeze n query indices (mod 2^lde_bits) into a..
 #define TOP_COPY 5          // challenge words a..a+n = words a-3r..  (lookup deltas := betas ++ gammas)
 #define TOP_ZERO 6          // challenge words a..a+n = 0
+
+// vanishing work items (host-built list; each is a contiguous run of the alpha-combined
+// term sequence, evaluated by one wave per 64 proofs)
+#define VI_ZS1 0      // the r Z(1) boundary terms
+#define VI_PP 1       // partial-product terms of challenge round a
+#define VI_LOOKUP 2   // lookup terms of challenge round a
+#define VI_GATE 3     // gate a, part b (PoseidonGate: 8 parts, others: 1)
+#define P2V_POSEIDON_PARTS 8
+// first term (in the gate's own numbering) of PoseidonGate part k (see vanish.hip)
+static inline constexpr int p2v_poseidon_part_first_term(int part) {
+  return part == 0 ? 0 : part <= 2 ? 17 + 12 * (part - 1) : part == 3 ? 41 : 75 + 12 * (part - 4);
+}
 
 // challenge buffer offsets (match the P2V_TRACE layout prefix in include/p2v.h)
 #define CH_PI(c) 0

@@ -68,6 +68,51 @@ GL_HD uint64_t reduce96_nc(uint64_t hi, uint64_t lo) {
   return r;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// gfx950 carry-chain primitives.  The compiler does not use the carry-out of
+// v_mad_u64_u32 / v_add_co_u32 and re-derives every carry with a 64-bit compare; these
+// wrappers expose the hardware carry (an SGPR-pair lane mask).  They are plain (non-volatile)
+// asm, so the scheduler still interleaves them, and it inserts the SGPR write->read hazard
+// waits between them itself.
+namespace ax {
+__device__ __forceinline__ uint64_t mad0(uint32_t a, uint32_t b) { uint64_t d, c; asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(d), "=s"(c) : "v"(a), "v"(b)); return d; }
+__device__ __forceinline__ uint64_t mad_co(uint32_t a, uint32_t b, uint64_t x, uint64_t& co) { uint64_t d; asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(a), "v"(b), "v"(x)); return d; }
+__device__ __forceinline__ uint64_t madm1_co(uint32_t a, uint64_t x, uint64_t& co) { uint64_t d; asm("v_mad_u64_u32 %0, %1, %2, -1, %3" : "=v"(d), "=s"(co) : "v"(a), "v"(x)); return d; }
+__device__ __forceinline__ uint32_t add_co(uint32_t a, uint32_t b, uint64_t& co) { uint32_t d; asm("v_add_co_u32_e64 %0, %1, %2, %3" : "=v"(d), "=s"(co) : "v"(a), "v"(b)); return d; }
+__device__ __forceinline__ uint32_t addc_co(uint32_t a, uint32_t b, uint64_t ci, uint64_t& co) { uint32_t d; asm("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(a), "v"(b), "s"(ci)); return d; }
+__device__ __forceinline__ uint32_t addc0(uint32_t a, uint64_t ci) { uint32_t d; uint64_t co; asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(d), "=s"(co) : "v"(a), "s"(ci)); return d; }
+__device__ __forceinline__ uint32_t sub_co(uint32_t a, uint32_t b, uint64_t& co) { uint32_t d; asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(d), "=s"(co) : "v"(a), "v"(b)); return d; }
+__device__ __forceinline__ uint32_t subb0_co(uint32_t a, uint64_t ci, uint64_t& co) { uint32_t d; asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(d), "=s"(co) : "v"(a), "s"(ci)); return d; }
+__device__ __forceinline__ uint32_t mask_m1(uint64_t m) { uint32_t d; asm("v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(d) : "s"(m)); return d; }
+__device__ __forceinline__ uint32_t mask_1(uint64_t m) { uint32_t d; asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(d) : "s"(m)); return d; }
+}  // namespace ax
+
+// a * b (mod p) for any a, b < 2^64, result in [0, 2^64) (not necessarily canonical).
+// 17 VALU: 4 partial products, the exact 128-bit product through the carry chain, then
+// lo + hi_lo (2^32 - 1) - hi_hi with one fix-up per wrap (2^64 == 2^32 - 1 mod p).
+__device__ __forceinline__ uint64_t mul_nc_dev(uint64_t a, uint64_t b) {
+  using namespace ax;
+  const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+  uint64_t cm, c1, c2, ct, c4, bw1, bw2, bw3, bw4;
+  const uint64_t p00 = mad0(a0, b0);
+  const uint64_t p01 = mad0(a0, b1);
+  const uint64_t m = mad_co(a1, b0, p01, cm);   // a0 b1 + a1 b0 = m + cm 2^64
+  const uint64_t p11 = mad0(a1, b1);
+  const uint32_t lo1 = add_co((uint32_t)(p00 >> 32), (uint32_t)m, c1);
+  const uint32_t h0 = addc_co((uint32_t)p11, (uint32_t)(m >> 32), c1, c2);
+  const uint32_t h1 = addc0((uint32_t)(p11 >> 32), c2) + mask_1(cm);   // exact: the product is < 2^128
+  const uint64_t lo = ((uint64_t)lo1 << 32) | (uint32_t)p00;
+  const uint64_t t = madm1_co(h0, lo, ct);                              // lo + h0 (2^32 - 1)
+  const uint32_t tl = add_co((uint32_t)t, mask_m1(ct), c4);             // wrapped: + 2^32 - 1
+  const uint32_t th = addc0((uint32_t)(t >> 32), c4);
+  const uint32_t rl = sub_co(tl, h1, bw1);                              // - h1
+  const uint32_t rh = subb0_co(th, bw1, bw2);
+  const uint32_t rl2 = sub_co(rl, mask_m1(bw2), bw3);                   // wrapped: - (2^32 - 1)
+  const uint32_t rh2 = subb0_co(rh, bw3, bw4);
+  return ((uint64_t)rh2 << 32) | rl2;
+}
+#endif
+
 GL_HD void mul128(uint64_t a, uint64_t b, uint64_t& hi, uint64_t& lo) {
 #if defined(__HIP_DEVICE_COMPILE__)
   uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
@@ -92,7 +137,13 @@ GL_HD uint64_t sub(uint64_t a, uint64_t b) {   // a, b canonical
   return (a < b) ? d + P : d;
 }
 GL_HD uint64_t neg(uint64_t a) { return a ? P - a : 0; }
-GL_HD uint64_t mul(uint64_t a, uint64_t b) { uint64_t hi, lo; mul128(a, b, hi, lo); return reduce128(hi, lo); }
+GL_HD uint64_t mul(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return canon(mul_nc_dev(a, b));
+#else
+  uint64_t hi, lo; mul128(a, b, hi, lo); return reduce128(hi, lo);
+#endif
+}
 GL_HD uint64_t sqr(uint64_t a) { return mul(a, a); }
 // multiply by a small constant c < 2^32
 GL_HD uint64_t mul_small(uint64_t a, uint32_t c) {

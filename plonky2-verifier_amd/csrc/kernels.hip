@@ -272,6 +272,7 @@ extern "C" __global__ void __launch_bounds__(256) k_fri(DevCircuit c) {
   const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int NPB = c.B >> 6;
   if (unit >= c.Q * NPB) return;
+  __builtin_amdgcn_s_setprio(2);   // side stream, concurrent with k_merkle (see k_vanish)
   const int pb = unit % NPB, q = unit / NPB;
   const int p = pb * 64 + lane;
   const int64_t base = c.q0 + (int64_t)q * c.qstride;

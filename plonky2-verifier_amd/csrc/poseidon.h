@@ -38,9 +38,13 @@ __host__ __device__ __forceinline__ uint64_t add_nc(uint64_t a, uint64_t b) {   
   return s + ((s < a) ? gl::EPS : 0);   // a + b - 2^64 + EPS < 2^64: no second carry
 }
 __host__ __device__ __forceinline__ uint64_t mul_nc(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return gl::mul_nc_dev(a, b);
+#else
   uint64_t hi, lo;
   gl::mul128(a, b, hi, lo);
   return gl::reduce128_nc(hi, lo);
+#endif
 }
 // x^7
 __host__ __device__ __forceinline__ uint64_t sbox(uint64_t x) {
@@ -56,6 +60,15 @@ __host__ __device__ __forceinline__ uint64_t sbox(uint64_t x) {
 #define P2_UNROLL _Pragma("GCC unroll 12")
 #endif
 
+// ah * 2^32 + al (al, ah < 2^43) -> [0, 2^64): with ah = ah_hi 2^32 + ah_lo the value is
+// ah_hi 2^64 + ah_lo 2^32 + al == ah_hi (2^32 - 1) + al + ah_lo 2^32 (mod p); the first two
+// terms stay below 2^44, so one wrap fix-up suffices (v_mad_u64_u32 + 3 VALU).
+__host__ __device__ __forceinline__ uint64_t mds_reduce(uint64_t al, uint64_t ah) {
+  const uint64_t t = (ah >> 32) * 0xFFFFFFFFULL + al;
+  const uint64_t r = t + (ah << 32);
+  return r + (r < t ? gl::EPS : 0);
+}
+
 // y = M x with M = circ + diag; inputs any value < 2^64, outputs < 2^64 (lazy).
 // Each row is sum_j c_j x_j with c_j < 2^6, accumulated separately over the 32-bit halves.
 __host__ __device__ __forceinline__ void mds(uint64_t s[12]) {
@@ -69,10 +82,7 @@ __host__ __device__ __forceinline__ void mds(uint64_t s[12]) {
       al += (uint64_t)(uint32_t)s[j] * c;
       ah += (s[j] >> 32) * c;
     }
-    // value = ah * 2^32 + al,  al, ah < 2^42
-    uint64_t l = al + (ah << 32);
-    uint64_t h = (ah >> 32) + (l < al ? 1 : 0);
-    out[i] = gl::reduce96_nc(h, l);
+    out[i] = mds_reduce(al, ah);
   }
   P2_UNROLL
   for (int i = 0; i < 12; i++) s[i] = out[i];

@@ -66,9 +66,7 @@ __device__ __forceinline__ void mds(uint64_t x[3], int t) {
         ah += (X[d][k] >> 32) * c;
       }
     }
-    uint64_t l = al + (ah << 32);
-    uint64_t h = (ah >> 32) + (l < al ? 1 : 0);
-    out[m] = gl::reduce96_nc(h, l);
+    out[m] = p2::mds_reduce(al, ah);
   }
 #pragma unroll
   for (int k = 0; k < 3; k++) x[k] = out[k];

@@ -58,86 +58,106 @@ struct Vars {
 
 __device__ __forceinline__ E esbox(E x) { E x2 = gl::emul(x, x); E x3 = gl::emul(x, x2); E x4 = gl::emul(x2, x2); return gl::emul(x3, x4); }
 
-// PoseidonGate, Gate/Custom/Poseidon.hs:63-150 (fast partial rounds)
-__device__ __noinline__ void gate_poseidon(const Vars& V, Acc& A) {
-  const E one = gl::eb(1);
-  const E swap = V.w(24);
-  A.push(gl::emul(swap, gl::esub(swap, one)));
-  for (int i = 0; i < 4; i++) A.push(gl::esub(gl::emul(swap, gl::esub(V.w(i + 4), V.w(i))), V.w(25 + i)));
-  E st[12];
-#pragma unroll
-  for (int i = 0; i < 4; i++) st[i] = gl::eadd(V.w(i), V.w(25 + i));
-#pragma unroll
-  for (int i = 4; i < 8; i++) st[i] = gl::esub(V.w(i), V.w(25 + i - 4));
-#pragma unroll
-  for (int i = 8; i < 12; i++) st[i] = V.w(i);
+// PoseidonGate, Gate/Custom/Poseidon.hs:63-150 (fast partial rounds), split into 8
+// independent parts so that one gate does not serialise a whole wave.  Within a full round
+// the state is replaced by the S-box witness wires, so the state entering full round r >= 2
+// (and the gate output) is MDS(sbox(wires of round r-1)): every full-round constraint block
+// can be evaluated from the wires alone.  Only the partial rounds form a chain.
+//   part 0: swap constraints + round 1 (terms [0,17))     part 1, 2: rounds 2, 3
+//   part 3: partial rounds + round 26 ([41,75))           part 4..6: rounds 27..29
+//   part 7: output ([111,123))
+// Term numbering is the gate's own (Acc starts at alpha^first_term of the part).
+__device__ __forceinline__ void mds_e(E st[12]) {
   E t[12];
-#pragma unroll 1
-  for (int r = 0; r < 4; r++) {
 #pragma unroll
-    for (int i = 0; i < 12; i++) st[i] = gl::eadd(st[i], lit(p2::c_round_constants[12 * r + i]));
-    if (r != 0) {
-#pragma unroll
-      for (int i = 0; i < 12; i++) { E sb = V.w(29 + 12 * (r - 1) + i); A.push(gl::esub(st[i], sb)); st[i] = sb; }
-    }
-#pragma unroll
-    for (int i = 0; i < 12; i++) st[i] = esbox(st[i]);
-#pragma unroll
-    for (int i = 0; i < 12; i++) {
-      E acc = gl::e0();
-#pragma unroll
-      for (int j = 0; j < 12; j++) acc = gl::eadd(acc, E{gl::mul_small(st[j].a, p2::mds_coeff(i, j)), gl::mul_small(st[j].b, p2::mds_coeff(i, j))});
-      t[i] = acc;
-    }
-#pragma unroll
-    for (int i = 0; i < 12; i++) st[i] = t[i];
-  }
-#pragma unroll
-  for (int i = 0; i < 12; i++) st[i] = gl::eadd(st[i], lit(p2::c_fast_first_rc[i]));
-  // mdsInitPartial: partialMdsMatrixCoeff i j = INITIAL_MATRIX ! (j, i)
-  t[0] = st[0];
-#pragma unroll
-  for (int i = 0; i < 11; i++) {
+  for (int i = 0; i < 12; i++) {
     E acc = gl::e0();
 #pragma unroll
-    for (int j = 0; j < 11; j++) acc = gl::eadd(acc, gl::escale(p2::c_fast_init_matrix[11 * j + i], st[1 + j]));
-    t[1 + i] = acc;
+    for (int j = 0; j < 12; j++) acc = gl::eadd(acc, E{gl::mul_small(st[j].a, p2::mds_coeff(i, j)), gl::mul_small(st[j].b, p2::mds_coeff(i, j))});
+    t[i] = acc;
   }
 #pragma unroll
   for (int i = 0; i < 12; i++) st[i] = t[i];
-#pragma unroll 1
-  for (int r = 0; r < 22; r++) {
-    const E sb = V.w(29 + 36 + r);
-    A.push(gl::esub(st[0], sb));
-    E z = esbox(sb);
-    if (r < 21) z = gl::eadd(z, lit(p2::c_fast_rc[r]));
-    // mdsFastPartial r
-    E d = E{gl::mul_small(z.a, p2::mds_coeff(0, 0)), gl::mul_small(z.b, p2::mds_coeff(0, 0))};
+}
+// state after a full round whose S-box inputs are the 12 wires starting at w0
+__device__ __forceinline__ void state_from_sbox_wires(const Vars& V, int w0, E st[12]) {
 #pragma unroll
-    for (int j = 0; j < 11; j++) d = gl::eadd(d, gl::escale(p2::c_fast_w_hats[11 * r + j], st[1 + j]));
+  for (int i = 0; i < 12; i++) st[i] = esbox(V.w(w0 + i));
+  mds_e(st);
+}
+// round r: st += rc(r); constraint st - wires[w0..w0+12)
+__device__ __forceinline__ void round_constraint(const Vars& V, Acc& A, E st[12], int r, int w0) {
 #pragma unroll
-    for (int j = 0; j < 11; j++) st[1 + j] = gl::eadd(st[1 + j], gl::escale(p2::c_fast_vs[11 * r + j], z));
-    st[0] = d;
+  for (int i = 0; i < 12; i++) A.push(gl::esub(gl::eadd(st[i], lit(p2::c_round_constants[12 * r + i])), V.w(w0 + i)));
+}
+
+constexpr int POS_SB1 = 29, POS_SBP = 29 + 36, POS_SBF = 29 + 36 + 22;
+
+__device__ __noinline__ void gate_poseidon(const Vars& V, Acc& A, int part) {
+  E st[12];
+  if (part == 0) {
+    const E one = gl::eb(1);
+    const E swap = V.w(24);
+    A.push(gl::emul(swap, gl::esub(swap, one)));
+    for (int i = 0; i < 4; i++) A.push(gl::esub(gl::emul(swap, gl::esub(V.w(i + 4), V.w(i))), V.w(25 + i)));
+#pragma unroll
+    for (int i = 0; i < 4; i++) st[i] = gl::eadd(V.w(i), V.w(25 + i));
+#pragma unroll
+    for (int i = 4; i < 8; i++) st[i] = gl::esub(V.w(i), V.w(25 + i - 4));
+#pragma unroll
+    for (int i = 8; i < 12; i++) st[i] = V.w(i);
+#pragma unroll
+    for (int i = 0; i < 12; i++) st[i] = esbox(gl::eadd(st[i], lit(p2::c_round_constants[i])));
+    mds_e(st);
+    round_constraint(V, A, st, 1, POS_SB1);
+    return;
   }
-#pragma unroll 1
-  for (int r = 0; r < 4; r++) {
+  if (part <= 2) {   // rounds 2, 3
+    const int r = part + 1;
+    state_from_sbox_wires(V, POS_SB1 + 12 * (r - 2), st);
+    round_constraint(V, A, st, r, POS_SB1 + 12 * (r - 1));
+    return;
+  }
+  if (part == 3) {   // partial rounds (fast form) + the round-26 constraint
+    state_from_sbox_wires(V, POS_SB1 + 24, st);
 #pragma unroll
-    for (int i = 0; i < 12; i++) {
-      st[i] = gl::eadd(st[i], lit(p2::c_round_constants[12 * (r + 26) + i]));
-      const E sb = V.w(29 + 36 + 22 + 12 * r + i);
-      A.push(gl::esub(st[i], sb));
-      st[i] = esbox(sb);
-    }
+    for (int i = 0; i < 12; i++) st[i] = gl::eadd(st[i], lit(p2::c_fast_first_rc[i]));
+    // mdsInitPartial: partialMdsMatrixCoeff i j = INITIAL_MATRIX ! (j, i)
+    E t[12];
+    t[0] = st[0];
 #pragma unroll
-    for (int i = 0; i < 12; i++) {
+    for (int i = 0; i < 11; i++) {
       E acc = gl::e0();
 #pragma unroll
-      for (int j = 0; j < 12; j++) acc = gl::eadd(acc, E{gl::mul_small(st[j].a, p2::mds_coeff(i, j)), gl::mul_small(st[j].b, p2::mds_coeff(i, j))});
-      t[i] = acc;
+      for (int j = 0; j < 11; j++) acc = gl::eadd(acc, gl::escale(p2::c_fast_init_matrix[11 * j + i], st[1 + j]));
+      t[1 + i] = acc;
     }
 #pragma unroll
     for (int i = 0; i < 12; i++) st[i] = t[i];
+#pragma unroll 1
+    for (int r = 0; r < 22; r++) {
+      const E sb = V.w(POS_SBP + r);
+      A.push(gl::esub(st[0], sb));
+      E z = esbox(sb);
+      if (r < 21) z = gl::eadd(z, lit(p2::c_fast_rc[r]));
+      // mdsFastPartial r
+      E d = E{gl::mul_small(z.a, p2::mds_coeff(0, 0)), gl::mul_small(z.b, p2::mds_coeff(0, 0))};
+#pragma unroll
+      for (int j = 0; j < 11; j++) d = gl::eadd(d, gl::escale(p2::c_fast_w_hats[11 * r + j], st[1 + j]));
+#pragma unroll
+      for (int j = 0; j < 11; j++) st[1 + j] = gl::eadd(st[1 + j], gl::escale(p2::c_fast_vs[11 * r + j], z));
+      st[0] = d;
+    }
+    round_constraint(V, A, st, 26, POS_SBF);
+    return;
   }
+  if (part <= 6) {   // rounds 27..29
+    const int r = 26 + part - 3;
+    state_from_sbox_wires(V, POS_SBF + 12 * (r - 27), st);
+    round_constraint(V, A, st, r, POS_SBF + 12 * (r - 26));
+    return;
+  }
+  state_from_sbox_wires(V, POS_SBF + 36, st);   // output
   for (int i = 0; i < 12; i++) A.push(gl::esub(st[i], V.w(i + 12)));
 }
 
@@ -233,7 +253,7 @@ __device__ __noinline__ void gate_random_access(const Vars& V, Acc& A, int nbits
   for (int64_t j = 0; j < extra; j++) A.push(gl::esub(V.k(j), V.w(copies * width + j)));
 }
 
-__device__ void eval_gate(const DevCircuit& c, const Vars& V, Acc& A, int g) {
+__device__ void eval_gate(const DevCircuit& c, const Vars& V, Acc& A, int g, int part) {
   const int kind = c.gate_kind[g];
   const int64_t p0 = c.gate_par[3 * g], p1 = c.gate_par[3 * g + 1], p2 = c.gate_par[3 * g + 2];
   const E one = gl::eb(1);
@@ -286,7 +306,7 @@ __device__ void eval_gate(const DevCircuit& c, const Vars& V, Acc& A, int g) {
     case 10:   // PublicInputGate, :88-89
       for (int i = 0; i < 4; i++) A.push(gl::esub(V.w(i), gl::eb(chal(c, CH_PI(c) + i, V.p))));
       break;
-    case 11: gate_poseidon(V, A); break;
+    case 11: gate_poseidon(V, A, part); break;
     case 12:   // PoseidonMdsGate, Custom/Poseidon.hs:49-59
       for (int i = 0; i < 12; i++) {
         EE acc = EE{gl::e0(), gl::e0()};
@@ -317,136 +337,173 @@ __device__ void eval_gate(const DevCircuit& c, const Vars& V, Acc& A, int g) {
   }
 }
 
-__device__ void vanish_lane(const DevCircuit& c, int p) {
-  const int r = c.r;
-  const E zeta = chal_e(c, CH_ZETA(c), p);
-  Acc T;   // main term sequence
-  T.r = r;
-#pragma unroll
-  for (int i = 0; i < P2V_MAX_R; i++) { T.h[i] = gl::e0(); T.pw[i] = 1; T.al[i] = i < r ? chal(c, CH_ALPHA(c) + i, p) : 0; }
-  const E one = gl::eb(1);
+__device__ __forceinline__ uint64_t pow_u(uint64_t x, uint32_t e) {   // uniform exponent
+  uint64_t acc = 1;
+  for (; e; e >>= 1) { if (e & 1) acc = gl::mul(acc, x); x = gl::mul(x, x); }
+  return acc;
+}
+
+// Z(1) boundary terms: L0(zeta)(Z_i(zeta) - 1), Vanishing.hs:86-95, Algebra/Poly.hs:14-16
+__device__ void item_zs1(const DevCircuit& c, Acc& T, int p) {
+  const E zeta = chal_e(c, CH_ZETA(c), p), one = gl::eb(1);
   const E zeta_n = epow2n(zeta, c.degree_bits);
-  // zs1: L0(zeta)(z - 1), Algebra/Poly.hs:14-16
   E L0;
   if (gl::eeq(zeta, one)) L0 = one;
   else L0 = gl::emul(gl::esub(zeta_n, one), einv(gl::escale((1ULL << c.degree_bits) % gl::P, gl::esub(zeta, one))));
-  for (int i = 0; i < r; i++) T.push(gl::emul(L0, gl::esub(lde(c, c.o_zs + 2 * i, p), one)));
-  // partial products, Vanishing.hs:97-111
-  for (int j = 0; j < r; j++) {
-    const uint64_t beta = chal(c, CH_BETA(c) + j, p), gamma = chal(c, CH_GAMMA(c) + j, p);
-    const int nnum = c.num_routed < c.num_wires ? c.num_routed : c.num_wires;
-    for (int ch = 0; ch < c.n_pp_terms; ch++) {
-      const E prev = ch == 0 ? lde(c, c.o_zs + 2 * j, p) : lde(c, c.o_pp + 2 * ((int64_t)j * c.npp + ch - 1), p);
-      const E next = ch == c.npp ? lde(c, c.o_zs_next + 2 * j, p) : lde(c, c.o_pp + 2 * ((int64_t)j * c.npp + ch), p);
-      E pn = one, pd = one;
-      for (int t = ch * c.qdf; t < nnum && t < (ch + 1) * c.qdf; t++) {
-        const E w = lde(c, c.o_wires + 2 * t, p);
-        pn = gl::emul(pn, gl::eadd(gl::eadd(w, gl::escale(gl::mul(beta, c.k_is[t]), zeta)), gl::eb(gamma)));
-        pd = gl::emul(pd, gl::eadd(gl::eadd(w, gl::escale(beta, lde(c, c.o_sig + 2 * t, p))), gl::eb(gamma)));
-      }
-      T.push(gl::esub(gl::emul(prev, pn), gl::emul(next, pd)));
+  for (int i = 0; i < c.r; i++) T.push(gl::emul(L0, gl::esub(lde(c, c.o_zs + 2 * i, p), one)));
+}
+
+// partial-product transitions of challenge round j, Vanishing.hs:97-111
+__device__ void item_pp(const DevCircuit& c, Acc& T, int j, int p) {
+  const E zeta = chal_e(c, CH_ZETA(c), p), one = gl::eb(1);
+  const uint64_t beta = chal(c, CH_BETA(c) + j, p), gamma = chal(c, CH_GAMMA(c) + j, p);
+  const int nnum = c.num_routed < c.num_wires ? c.num_routed : c.num_wires;
+  for (int ch = 0; ch < c.n_pp_terms; ch++) {
+    const E prev = ch == 0 ? lde(c, c.o_zs + 2 * j, p) : lde(c, c.o_pp + 2 * ((int64_t)j * c.npp + ch - 1), p);
+    const E next = ch == c.npp ? lde(c, c.o_zs_next + 2 * j, p) : lde(c, c.o_pp + 2 * ((int64_t)j * c.npp + ch), p);
+    E pn = one, pd = one;
+    for (int t = ch * c.qdf; t < nnum && t < (ch + 1) * c.qdf; t++) {
+      const E w = lde(c, c.o_wires + 2 * t, p);
+      pn = gl::emul(pn, gl::eadd(gl::eadd(w, gl::escale(gl::mul(beta, c.k_is[t]), zeta)), gl::eb(gamma)));
+      pd = gl::emul(pd, gl::eadd(gl::eadd(w, gl::escale(beta, lde(c, c.o_sig + 2 * t, p))), gl::eb(gamma)));
     }
+    T.push(gl::esub(gl::emul(prev, pn), gl::emul(next, pd)));
   }
-  // lookups, Plonk/Lookups.hs:45-132
-  if (c.nluts > 0) {
-    const int nlp = c.nlp, nsldc = nlp - 1;
-    const int nlu = c.num_routed / 2 < c.num_wires / 2 ? c.num_routed / 2 : c.num_wires / 2;
-    const int slots3 = c.num_routed / 3;
-    const int nlut = slots3 < c.num_wires / 3 ? slots3 : c.num_wires / 3;
-    const int lu_degree = c.qdf - 1, lut_degree = (slots3 + nsldc - 1) / nsldc;
-    const int nclu = (nlu + lu_degree - 1) / lu_degree, nclut = (nlut + lut_degree - 1) / lut_degree, ncm = (slots3 + lut_degree - 1) / lut_degree;
-    int nz = nclu < nclut ? nclu : nclut; nz = nz < ncm ? nz : ncm; nz = nz < nsldc ? nz : nsldc;
-    const int64_t ls = c.o_const + 2 * (int64_t)c.ngroups;   // lookup selectors
-    auto sel = [&](int k) { return lde(c, ls + 2 * k, p); };
-    auto wv = [&](int t) { return lde(c, c.o_wires + 2 * (int64_t)t, p); };
-    for (int j = 0; j < r; j++) {
-      const uint64_t dA = chal(c, CH_DELTA(c) + 4 * j, p), dB = chal(c, CH_DELTA(c) + 4 * j + 1, p);
-      const uint64_t dal = chal(c, CH_DELTA(c) + 4 * j + 2, p), dde = chal(c, CH_DELTA(c) + 4 * j + 3, p);
-      const int64_t zoff = c.o_lzs + 2 * (int64_t)j * nlp, znoff = c.o_lzs_next + 2 * (int64_t)j * nlp;
-      const E re = lde(c, zoff, p), re_next = lde(c, znoff, p);
-      auto sldc = [&](int k) { return lde(c, zoff + 2 * (1 + k), p); };
-      auto sldc_next = [&](int k) { return lde(c, znoff + 2 * (1 + k), p); };
-      T.push(gl::emul(sel(3), sldc(nsldc - 1)));
-      T.push(gl::emul(sel(2), sldc(0)));
-      T.push(gl::emul(sel(2), re));
-      for (int k = 0; k < c.nluts; k++) {   // evalFinalRE, :103-109
-        const int64_t len = c.lut_len[k], off = c.lut_off[k];
-        const int64_t padded = ((len + slots3 - 1) / slots3) * slots3;
-        uint64_t cur = 0;
-        for (int64_t i = 0; i < padded; i++) {
-          const int64_t jj = i < len ? i : 0;
-          cur = gl::add(gl::mul(dde, cur), gl::add(c.lut_in[off + jj], gl::mul(dB, c.lut_out[off + jj])));
-        }
-        T.push(gl::emul(sel(4 + k), gl::esub(re, gl::eb(cur))));
-      }
-      {
-        E cs = re_next;
-        for (int t = 0; t < nlut; t++) cs = gl::eadd(gl::escale(dde, cs), gl::eadd(wv(3 * t), gl::escale(dB, wv(3 * t + 1))));
-        T.push(gl::emul(sel(0), gl::esub(re, cs)));
-      }
-      const E alpha = gl::eb(dal);
-      for (int ch = 0; ch < nz; ch++) {
-        const E prev = ch == 0 ? sldc_next(nsldc - 1) : sldc(ch - 1);
-        const E curv = sldc(ch);
-        E Plu = one, Slu = gl::e0(), Plut = one, Slut = gl::e0();
-        const int lus = ch * lu_degree, lue = (lus + lu_degree < nlu) ? lus + lu_degree : nlu;
-        for (int t = lus; t < lue; t++) {
-          const E x = gl::esub(alpha, gl::eadd(wv(2 * t), gl::escale(dA, wv(2 * t + 1))));
-          Slu = gl::eadd(gl::emul(Slu, x), Plu); Plu = gl::emul(Plu, x);
-        }
-        const int tts = ch * lut_degree, tte = (tts + lut_degree < nlut) ? tts + lut_degree : nlut;
-        const int mte = (tts + lut_degree < slots3) ? tts + lut_degree : slots3;
-        const int nmz = (tte - tts) < (mte - tts) ? (tte - tts) : (mte - tts);
-        for (int t = tts; t < tte; t++) {
-          const E y = gl::esub(alpha, gl::eadd(wv(3 * t), gl::escale(dA, wv(3 * t + 1))));
-          const E m = (t - tts) < nmz ? wv(3 * t + 2) : gl::e0();
-          Slut = gl::eadd(gl::emul(Slut, y), gl::emul(m, Plut)); Plut = gl::emul(Plut, y);
-        }
-        const E diff = gl::esub(curv, prev);
-        T.push(gl::emul(sel(0), gl::esub(gl::emul(Plut, diff), Slut)));   // eq_sum_trans
-        T.push(gl::emul(sel(1), gl::eadd(gl::emul(Plu, diff), Slu)));     // eq_ldc_trans
-      }
+}
+
+// lookup terms of challenge round j, Plonk/Lookups.hs:45-132
+__device__ void item_lookup(const DevCircuit& c, Acc& T, int j, int p) {
+  const E one = gl::eb(1);
+  const int nlp = c.nlp, nsldc = nlp - 1;
+  const int nlu = c.num_routed / 2 < c.num_wires / 2 ? c.num_routed / 2 : c.num_wires / 2;
+  const int slots3 = c.num_routed / 3;
+  const int nlut = slots3 < c.num_wires / 3 ? slots3 : c.num_wires / 3;
+  const int lu_degree = c.qdf - 1, lut_degree = (slots3 + nsldc - 1) / nsldc;
+  const int nclu = (nlu + lu_degree - 1) / lu_degree, nclut = (nlut + lut_degree - 1) / lut_degree, ncm = (slots3 + lut_degree - 1) / lut_degree;
+  int nz = nclu < nclut ? nclu : nclut; nz = nz < ncm ? nz : ncm; nz = nz < nsldc ? nz : nsldc;
+  const int64_t ls = c.o_const + 2 * (int64_t)c.ngroups;   // lookup selectors
+  auto sel = [&](int k) { return lde(c, ls + 2 * k, p); };
+  auto wv = [&](int t) { return lde(c, c.o_wires + 2 * (int64_t)t, p); };
+  const uint64_t dA = chal(c, CH_DELTA(c) + 4 * j, p), dB = chal(c, CH_DELTA(c) + 4 * j + 1, p);
+  const uint64_t dal = chal(c, CH_DELTA(c) + 4 * j + 2, p), dde = chal(c, CH_DELTA(c) + 4 * j + 3, p);
+  const int64_t zoff = c.o_lzs + 2 * (int64_t)j * nlp, znoff = c.o_lzs_next + 2 * (int64_t)j * nlp;
+  const E re = lde(c, zoff, p), re_next = lde(c, znoff, p);
+  auto sldc = [&](int k) { return lde(c, zoff + 2 * (1 + k), p); };
+  auto sldc_next = [&](int k) { return lde(c, znoff + 2 * (1 + k), p); };
+  T.push(gl::emul(sel(3), sldc(nsldc - 1)));
+  T.push(gl::emul(sel(2), sldc(0)));
+  T.push(gl::emul(sel(2), re));
+  for (int k = 0; k < c.nluts; k++) {   // evalFinalRE, :103-109
+    const int64_t len = c.lut_len[k], off = c.lut_off[k];
+    const int64_t padded = ((len + slots3 - 1) / slots3) * slots3;
+    uint64_t cur = 0;
+    for (int64_t i = 0; i < padded; i++) {
+      const int64_t jj = i < len ? i : 0;
+      cur = gl::add(gl::mul(dde, cur), gl::add(c.lut_in[off + jj], gl::mul(dB, c.lut_out[off + jj])));
     }
+    T.push(gl::emul(sel(4 + k), gl::esub(re, gl::eb(cur))));
   }
-  // gates: alpha^G0 * sel_g * sum_k alpha^k c_gk
-  uint64_t base_pw[P2V_MAX_R];
+  {
+    E cs = re_next;
+    for (int t = 0; t < nlut; t++) cs = gl::eadd(gl::escale(dde, cs), gl::eadd(wv(3 * t), gl::escale(dB, wv(3 * t + 1))));
+    T.push(gl::emul(sel(0), gl::esub(re, cs)));
+  }
+  const E alpha = gl::eb(dal);
+  for (int ch = 0; ch < nz; ch++) {
+    const E prev = ch == 0 ? sldc_next(nsldc - 1) : sldc(ch - 1);
+    const E curv = sldc(ch);
+    E Plu = one, Slu = gl::e0(), Plut = one, Slut = gl::e0();
+    const int lus = ch * lu_degree, lue = (lus + lu_degree < nlu) ? lus + lu_degree : nlu;
+    for (int t = lus; t < lue; t++) {
+      const E x = gl::esub(alpha, gl::eadd(wv(2 * t), gl::escale(dA, wv(2 * t + 1))));
+      Slu = gl::eadd(gl::emul(Slu, x), Plu); Plu = gl::emul(Plu, x);
+    }
+    const int tts = ch * lut_degree, tte = (tts + lut_degree < nlut) ? tts + lut_degree : nlut;
+    const int mte = (tts + lut_degree < slots3) ? tts + lut_degree : slots3;
+    const int nmz = (tte - tts) < (mte - tts) ? (tte - tts) : (mte - tts);
+    for (int t = tts; t < tte; t++) {
+      const E y = gl::esub(alpha, gl::eadd(wv(3 * t), gl::escale(dA, wv(3 * t + 1))));
+      const E m = (t - tts) < nmz ? wv(3 * t + 2) : gl::e0();
+      Slut = gl::eadd(gl::emul(Slut, y), gl::emul(m, Plut)); Plut = gl::emul(Plut, y);
+    }
+    const E diff = gl::esub(curv, prev);
+    T.push(gl::emul(sel(0), gl::esub(gl::emul(Plut, diff), Slut)));   // eq_sum_trans
+    T.push(gl::emul(sel(1), gl::eadd(gl::emul(Plu, diff), Slu)));     // eq_ldc_trans
+  }
+}
+
+// One vanishing work item for proof p: a contiguous run of terms of the combined sequence
+// sum_k alpha_i^k t_k (Vanishing.hs:48-137).  Item `it` = {type, a, b, first_term}; its
+// partial sums (one F^2 per challenge round) go to vparts[it][2r][B].
+__device__ void vanish_item(const DevCircuit& c, int it, int p) {
+  const int type = c.vitems[4 * it], a = c.vitems[4 * it + 1], b = c.vitems[4 * it + 2];
+  const uint32_t first = (uint32_t)c.vitems[4 * it + 3];
+  const int r = c.r;
+  Acc T;
+  T.r = r;
 #pragma unroll
-  for (int i = 0; i < P2V_MAX_R; i++) base_pw[i] = T.pw[i];
-  Acc G;
-  G.r = r;
-#pragma unroll
-  for (int i = 0; i < P2V_MAX_R; i++) G.al[i] = T.al[i];
-  Vars V{&c, p};
-  const E unused = gl::eb(0xFFFFFFFFULL);
-  for (int g = 0; g < c.n_gates; g++) {
-    const int grp = c.gate_grp[g];
+  for (int i = 0; i < P2V_MAX_R; i++) {
+    T.h[i] = gl::e0();
+    T.al[i] = i < r ? chal(c, CH_ALPHA(c) + i, p) : 0;
+    T.pw[i] = i < r ? pow_u(T.al[i], first) : 0;
+  }
+  if (type == VI_ZS1) item_zs1(c, T, p);
+  else if (type == VI_PP) item_pp(c, T, a, p);
+  else if (type == VI_LOOKUP) item_lookup(c, T, a, p);
+  else {   // gate a (part b): alpha^G0 * S_g(zeta) * sum_k alpha^k c_gk, Vanishing.hs:113-125
+    const int grp = c.gate_grp[a];
     const E x = lde(c, c.o_const + 2 * grp, p);   // S_grp(zeta)
+    const E one = gl::eb(1);
+    const E unused = gl::eb(0xFFFFFFFFULL);
     E s = c.ngroups > 1 ? gl::esub(unused, x) : one;   // Gate/Selector.hs:83-89
-    for (int j = c.grp_start[grp]; j < c.grp_end[grp]; j++) if (j != g) s = gl::emul(s, gl::esub(gl::eb((uint64_t)j), x));
-    G.reset();
-    eval_gate(c, V, G, g);
+    for (int j = c.grp_start[grp]; j < c.grp_end[grp]; j++) if (j != a) s = gl::emul(s, gl::esub(gl::eb((uint64_t)j), x));
+    Vars V{&c, p};
+    eval_gate(c, V, T, a, b);
 #pragma unroll
-    for (int i = 0; i < P2V_MAX_R; i++) if (i < r) T.h[i] = gl::eadd(T.h[i], gl::escale(base_pw[i], gl::emul(s, G.h[i])));
+    for (int i = 0; i < P2V_MAX_R; i++)
+      if (i < r) T.h[i] = gl::escale(pow_u(T.al[i], (uint32_t)c.alpha_base_gates), gl::emul(s, T.h[i]));
   }
-  // Q(zeta) (zeta^n - 1) == C(zeta), Plonk/Verifier.hs:35-51
-  bool ok = true;
-  const E zn1 = gl::esub(zeta_n, one);
-  for (int i = 0; i < r; i++) {
-    E q = gl::e0();
-    for (int k = c.qdf - 1; k >= 0; k--) q = gl::eadd(gl::emul(q, zeta_n), lde(c, c.o_quot + 2 * ((int64_t)i * c.qdf + k), p));
-    ok = ok && gl::eeq(gl::emul(q, zn1), T.h[i]);
-    c.van[(int64_t)(1 + 2 * i) * c.B + p] = T.h[i].a;
-    c.van[(int64_t)(2 + 2 * i) * c.B + p] = T.h[i].b;
-    c.van[(int64_t)(1 + 2 * r + 2 * i) * c.B + p] = q.a;
-    c.van[(int64_t)(2 + 2 * r + 2 * i) * c.B + p] = q.b;
-  }
-  c.van[p] = ok ? 1 : 0;
+  uint64_t* dst = c.vparts + (int64_t)it * 2 * r * c.B + p;
+  for (int i = 0; i < r; i++) { dst[(int64_t)(2 * i) * c.B] = T.h[i].a; dst[(int64_t)(2 * i + 1) * c.B] = T.h[i].b; }
 }
 
 }  // namespace
 
+// one wave = (item, 64 proofs); items are wave-uniform, heaviest first (host order)
 extern "C" __global__ void __launch_bounds__(256) k_vanish(DevCircuit c) {
+  const int lane = threadIdx.x & 63;
+  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int NPB = c.B >> 6;
+  if (unit >= c.n_vitems * NPB) return;
+  const int it = unit / NPB, p = (unit % NPB) * 64 + lane;
+  // runs concurrently with k_merkle (VALU-bound, many waves): raise the priority of these
+  // few latency-bound waves so they do not end up on the critical path
+  __builtin_amdgcn_s_setprio(2);
+  vanish_item(c, it, p);
+}
+
+// sum of the item partials, then Q(zeta)(zeta^n - 1) == C(zeta), Plonk/Verifier.hs:35-51
+extern "C" __global__ void __launch_bounds__(256) k_vanish_final(DevCircuit c) {
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= c.B) return;
-  vanish_lane(c, p);
+  const int r = c.r;
+  const E one = gl::eb(1);
+  const E zeta_n = epow2n(chal_e(c, CH_ZETA(c), p), c.degree_bits);
+  const E zn1 = gl::esub(zeta_n, one);
+  bool ok = true;
+  for (int i = 0; i < r; i++) {
+    E h = gl::e0();
+    for (int it = 0; it < c.n_vitems; it++) {
+      const uint64_t* src = c.vparts + ((int64_t)it * 2 * r + 2 * i) * c.B + p;
+      h = gl::eadd(h, E{src[0], src[c.B]});
+    }
+    E q = gl::e0();
+    for (int k = c.qdf - 1; k >= 0; k--) q = gl::eadd(gl::emul(q, zeta_n), lde(c, c.o_quot + 2 * ((int64_t)i * c.qdf + k), p));
+    ok = ok && gl::eeq(gl::emul(q, zn1), h);
+    c.van[(int64_t)(1 + 2 * i) * c.B + p] = h.a;
+    c.van[(int64_t)(2 + 2 * i) * c.B + p] = h.b;
+    c.van[(int64_t)(1 + 2 * r + 2 * i) * c.B + p] = q.a;
+    c.van[(int64_t)(2 + 2 * r + 2 * i) * c.B + p] = q.b;
+  }
+  c.van[p] = ok ? 1 : 0;
 }
