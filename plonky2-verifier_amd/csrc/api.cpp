@@ -3,6 +3,7 @@
 // (reference src/Plonk/Verifier.hs:56-65), batched, on MI355X.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -12,7 +13,7 @@
 #include "gl.h"
 
 extern "C" __global__ void k_transpose(const uint64_t*, int64_t, int, uint64_t*, int);
-extern "C" __global__ void k_phase1(DevCircuit, int);
+extern "C" __global__ void k_phase1(DevCircuit, int, int);
 extern "C" __global__ void k_merkle(DevCircuit);
 extern "C" __global__ void k_fri(DevCircuit);
 extern "C" __global__ void k_vanish(DevCircuit);
@@ -64,6 +65,8 @@ struct p2v_verifier {
   hipStream_t side = nullptr;
   float last_ms[kNumKernels] = {0};
   bool timed = false;
+  int transcript_mode = 0;          // 0 auto, 1 row, 2 quad (env P2V_TRANSCRIPT)
+  int quad_min_batch = 2048;        // auto: quad form from this batch size on
 };
 
 extern "C" {
@@ -145,6 +148,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   auto* v = new p2v_verifier();
   v->circ = pc; v->device = device; v->max_batch = max_batch;
   v->Bmax = (max_batch + 63) / 64 * 64;
+  if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : 0;
   DevCircuit& d = v->dc;
   memset(&d, 0, sizeof d);
   d.r = C.r; d.Q = C.num_queries; d.S = (int)C.arities.size(); d.T = 4 + d.S;
@@ -291,10 +295,16 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   T1(0, st);
   // phase 1: transcript waves + leaf-hash waves in one launch (the leaf sponges do not
   // depend on the challenges, so they fill the GPU while the serial transcripts run)
-  const int nt_blocks = (4 * d.B + 255) / 256;   // 4 lanes per proof
+  // transcript form: the row form (16 lanes/proof) has the lowest latency, the quad form
+  // (4 lanes/proof) the lowest total cost; large batches hide the quad latency behind
+  // their leaf hashing.  P2V_TRANSCRIPT=row|quad overrides (measurement).
+  int tl = d.B >= v->quad_min_batch ? 4 : 16;
+  if (v->transcript_mode == 1) tl = 16;
+  else if (v->transcript_mode == 2) tl = 4;
+  const int nt_blocks = (tl * d.B + 255) / 256;
   const int leaf_units = d.Q * d.T * NPB;
   T0(1, st);
-  k_phase1<<<nt_blocks + (leaf_units + 3) / 4, 256, 0, st>>>(d, nt_blocks);
+  k_phase1<<<nt_blocks + (leaf_units + 3) / 4, 256, 0, st>>>(d, nt_blocks, tl);
   T1(1, st);
   // phase 2: Merkle paths on the main stream; FRI queries and the vanishing kernel (few,
   // long-latency waves) on the side stream, concurrently

@@ -7,7 +7,7 @@
 // control flow never diverges, and the Poseidon round constants are scalar operands.
 //
 //   k_transpose   proof-major -> SoA
-//   k_phase1      transcript waves (one lane per proof, ~114 sequential permutations,
+//   k_phase1      transcript waves (a row or quad of lanes per proof, ~115 sequential permutations,
 //                 Challenge/Verifier.hs:58-103 + Challenge/FRI.hs:65-104) run in the SAME
 //                 launch as the leaf-hash waves (one lane per (proof, query, tree) sponge,
 //                 Hash/Sponge.hs:26-31) which do not depend on the challenges
@@ -18,6 +18,7 @@
 //   k_status      reference evaluation order -> int8 status (+ optional trace)
 #include "devcommon.h"
 #include "qposeidon.h"
+#include "rposeidon.h"
 
 using namespace p2d;
 using gl::E;
@@ -66,9 +67,108 @@ __device__ __forceinline__ void leaf_hash_unit(const DevCircuit& c, int unit, in
 
 // The transcript (Challenge/Verifier.hs:58-103, Challenge/FRI.hs:65-104) is a fixed
 // sequence of absorbs and squeezes for a given circuit; the host compiles it into an op
-// program and this loop interprets it with ONE permutation call site.  Each proof's
-// duplex state is spread over a lane quad (qposeidon.h): the ~114 permutations form a
-// strictly serial chain, so per-permutation latency, not throughput, is what counts.
+// program and this loop interprets it with ONE permutation call site.  Each proof's duplex
+// state is spread over a 16-lane row (rposeidon.h): the ~115 permutations form a strictly
+// serial chain, so per-permutation latency, not throughput, is what counts.  Lane L owns
+// state word L, so an absorbed chunk is one load per lane, issued before the pending
+// permutation so that its latency hides behind it.
+template <int D>
+__device__ __forceinline__ uint64_t row_up(uint64_t v, bool plus) {   // value of lane L + D (mod 16)
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  const uint32_t l = plus ? rp::ror32<D>(lo) : rp::ror32<16 - D>(lo);
+  const uint32_t h = plus ? rp::ror32<D>(hi) : rp::ror32<16 - D>(hi);
+  return ((uint64_t)h << 32) | l;
+}
+template <int D>
+__device__ __forceinline__ E row_fold(E h, E ad, bool plus) {   // h_L + alpha^D h_{L+D}
+  return gl::eadd(h, gl::emul(ad, E{row_up<D>(h.a, plus), row_up<D>(h.b, plus)}));
+}
+
+__device__ __forceinline__ void transcript_row(const DevCircuit& c, int p, const rp::Row& R) {
+  const int L = R.L;
+  // public inputs hash, Hash/Sponge.hs:26-31 (sponge [] = zero digest)
+  uint64_t x = 0;
+  for (int i = 0; i < c.num_pis; i += 8) {
+    const int k = c.num_pis - i;
+    if (L < 8 && L < k) x = ld(c, c.pis + i + L, p);
+    x = rp::permute(x, R);
+  }
+  uint64_t pih[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    pih[w] = rp::get_word(x, w);
+    if (L == 0) chal(c, CH_PI(c) + w, p) = pih[w];
+  }
+  x = 0;
+  int nbuf = 0, outpos = -1;
+  bool absorbing = true;
+  const uint64_t qmask = (1ULL << c.lde_bits) - 1;
+  uint64_t fa0 = 0, fa1 = 0;   // FRI alpha, kept in registers for the reduced openings below
+  for (int o = 0; o < c.ntops; o++) {
+    const int type = c.tops[3 * o], a = c.tops[3 * o + 1], n = c.tops[3 * o + 2];
+    if (type == TOP_COPY) {   // mkLookupDeltaList (betas ++ gammas ++ ...), Challenge/Verifier.hs:36-40,82-86
+      if (L == 0) for (int k = 0; k < n; k++) chal(c, a + k, p) = chal(c, a - 3 * c.r + k, p);
+      continue;
+    }
+    if (type == TOP_ZERO) {
+      if (L == 0) for (int k = 0; k < n; k++) chal(c, a + k, p) = 0;
+      continue;
+    }
+    if (type <= TOP_ABSORB_DIGEST) {   // absorb n words, chunk by chunk (lazy duplex, Challenge/Pure.hs:38-69)
+      if (!absorbing) { absorbing = true; nbuf = 0; }
+      for (int k = 0; k < n;) {
+        const int start = nbuf == 8 ? 0 : nbuf;
+        const int take = (8 - start) < (n - k) ? (8 - start) : (n - k);
+        const int j = k + L - start;   // this lane's word of the chunk
+        const bool mine = L >= start && L < start + take;
+        uint64_t v = 0;
+        if (type == TOP_ABSORB_SOA) { if (mine) v = ld(c, (int64_t)a + j, p); }
+        else if (type == TOP_ABSORB_PIH) { const int w = j & 3; v = w == 0 ? pih[0] : w == 1 ? pih[1] : w == 2 ? pih[2] : pih[3]; }
+        else v = c.digest[j & 3];
+        if (nbuf == 8) { x = rp::permute(x, R); nbuf = 0; }   // overwrite mode: the rate part is replaced
+        if (mine) x = v;
+        nbuf += take;
+        k += take;
+      }
+      continue;
+    }
+    for (int k = 0; k < n; k++) {   // squeeze: output order state[7], state[6], ... (reverse of take 8)
+      if (absorbing || outpos < 0) { x = rp::permute(x, R); absorbing = false; outpos = 7; }
+      uint64_t w = rp::get_word(x, outpos);
+      outpos--;
+      if (type == TOP_SQUEEZE_IDX) w &= qmask;
+      if (a + k == CH_FRI_ALPHA(c)) fa0 = w;
+      if (a + k == CH_FRI_ALPHA(c) + 1) fa1 = w;
+      if (L == 0) chal(c, a + k, p) = w;
+    }
+  }
+  // precomputeReducedOpenings, Plonk/FRI.hs:128-134: Y = sum alpha^i y_i.  Split over the
+  // row: lane L sums the terms i = L (mod 16) in powers of alpha^16, then a 4-level DPP tree
+  // forms sum_L alpha^L H_L in lane 0.
+  const E alpha{fa0, fa1};
+  const E a2 = gl::emul(alpha, alpha), a4 = gl::emul(a2, a2), a8 = gl::emul(a4, a4), a16 = gl::emul(a8, a8);
+#pragma unroll
+  for (int b = 0; b < 2; b++) {
+    const int64_t n = b == 0 ? c.n_this : c.n_next, off = b == 0 ? c.o_const : c.o_zs_next;
+    const int64_t M = (n + 15) / 16;
+    E h = gl::e0();
+    for (int64_t m = M - 1; m >= 0; m--) {
+      const int64_t i = 16 * m + L;
+      const E y = i < n ? lde(c, off + 2 * i, p) : gl::e0();
+      h = gl::eadd(gl::emul(h, a16), y);
+    }
+    h = row_fold<1>(h, alpha, R.plus);
+    h = row_fold<2>(h, a2, R.plus);
+    h = row_fold<4>(h, a4, R.plus);
+    h = row_fold<8>(h, a8, R.plus);
+    if (L == 0) { chal(c, (b == 0 ? CH_Y0(c) : CH_Y1(c)), p) = h.a; chal(c, (b == 0 ? CH_Y0(c) : CH_Y1(c)) + 1, p) = h.b; }
+  }
+}
+
+// Quad form of the same transcript (qposeidon.h: 4 lanes per proof, 3 state words per
+// lane).  Higher per-permutation latency than the row form but ~2.3x fewer issue slots in
+// total, which is what matters once the batch is large enough that the transcript hides
+// behind the leaf hashing sharing its launch (the host picks the form, see api.cpp).
 __device__ __forceinline__ void transcript_quad(const DevCircuit& c, int p, int t) {
   // public inputs hash, Hash/Sponge.hs:26-31 (sponge [] = zero digest)
   uint64_t x[3] = {0, 0, 0};
@@ -152,16 +252,21 @@ __device__ __forceinline__ void transcript_quad(const DevCircuit& c, int p, int 
 }
 
 // ------------------------------------------------------------------------ phase 1
-// blocks [0, nt_blocks): transcript quads (64 proofs per block, 4 lanes each, at raised
-// wave priority so co-resident leaf waves do not stretch the serial chain); the rest:
-// leaf hashing, 4 units per block.  Transcript blocks come first so they start first.
-extern "C" __global__ void __launch_bounds__(256) k_phase1(DevCircuit c, int nt_blocks) {
+// blocks [0, nt_blocks): transcripts, `tl` lanes per proof (16: row form, 4: quad form) at
+// raised wave priority so co-resident leaf waves do not stretch the serial chain; the
+// rest: leaf hashing, 4 units per block.  Transcript blocks come first so they start first.
+extern "C" __global__ void __launch_bounds__(256) k_phase1(DevCircuit c, int nt_blocks, int tl) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if ((int)blockIdx.x < nt_blocks) {
     __builtin_amdgcn_s_setprio(3);
     const int g = blockIdx.x * 256 + threadIdx.x;
-    const int p = g >> 2, t = g & 3;
-    if (p < c.B) transcript_quad(c, p, t);
+    if (tl == 16) {
+      rp::Row R;
+      rp::init(R, threadIdx.x);
+      if ((g >> 4) < c.B) transcript_row(c, g >> 4, R);
+    } else {
+      if ((g >> 2) < c.B) transcript_quad(c, g >> 2, g & 3);
+    }
     return;
   }
   const int unit = ((int)blockIdx.x - nt_blocks) * 4 + wave;

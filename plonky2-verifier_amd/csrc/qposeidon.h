@@ -37,14 +37,13 @@ __device__ __forceinline__ uint64_t bcast64(uint64_t v, int src) {
   return ((uint64_t)bcast32((uint32_t)(v >> 32), src) << 32) | bcast32((uint32_t)v, src);
 }
 
-// this lane's round constant for word 3t+k of round r: scalar loads + lane selects
+// this lane's round constants (words 3t..3t+2 of round r): in the natural table layout
+// (Hash/Constants.hs) they are contiguous, so each lane does a plain vector load.  The caller
+// prefetches one round ahead so the load latency hides behind the current round.
 __device__ __forceinline__ void lane_rc(int r, int t, uint64_t rc[3]) {
-  const uint64_t* R = p2::c_round_constants + 12 * r;
+  const uint64_t* R = p2::c_round_constants + 12 * r + 3 * t;
 #pragma unroll
-  for (int k = 0; k < 3; k++) {
-    const uint64_t a = R[k], b = R[3 + k], c = R[6 + k], d = R[9 + k];
-    rc[k] = t == 0 ? a : t == 1 ? b : t == 2 ? c : d;
-  }
+  for (int k = 0; k < 3; k++) rc[k] = R[k];
 }
 
 __device__ __forceinline__ void mds(uint64_t x[3], int t) {
@@ -74,10 +73,13 @@ __device__ __forceinline__ void mds(uint64_t x[3], int t) {
 
 // the quad's permutation; x = this lane's three words (inputs < 2^64, outputs canonical)
 __device__ __forceinline__ void permute(uint64_t x[3], int t) {
-  uint64_t rc[3];
+  uint64_t rc[3], nrc[3];
+  lane_rc(0, t, nrc);
 #pragma unroll 1
   for (int r = 0; r < 30; r++) {
-    lane_rc(r, t, rc);
+#pragma unroll
+    for (int k = 0; k < 3; k++) rc[k] = nrc[k];
+    lane_rc(r < 29 ? r + 1 : 29, t, nrc);
     const bool full = r < 4 || r >= 26;
     if (full) {
 #pragma unroll
