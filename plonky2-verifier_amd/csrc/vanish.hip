@@ -464,7 +464,9 @@ __device__ void vanish_item(const DevCircuit& c, int it, int p) {
       if (i < r) T.h[i] = gl::escale(pow_u(T.al[i], (uint32_t)c.alpha_base_gates), gl::emul(s, T.h[i]));
   }
   uint64_t* dst = c.vparts + (int64_t)it * 2 * r * c.B + p;
-  for (int i = 0; i < r; i++) { dst[(int64_t)(2 * i) * c.B] = T.h[i].a; dst[(int64_t)(2 * i + 1) * c.B] = T.h[i].b; }
+#pragma unroll
+  for (int i = 0; i < P2V_MAX_R; i++)   // constant indices: T stays in registers
+    if (i < r) { dst[(int64_t)(2 * i) * c.B] = T.h[i].a; dst[(int64_t)(2 * i + 1) * c.B] = T.h[i].b; }
 }
 
 }  // namespace

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Summarise a profile_round.sh run into profiles/.
+
+- <tag>_kernel_stats.csv          rocprofv3 --kernel-trace --stats of the default bench command
+- <tag>_kernel_stats_serial.csv   the same with --inflight 1 (averages = bench's kernel_ms)
+- pmc_traffic.json                HBM bytes per launch per kernel from the two PMC passes,
+                                  bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (MI355X_MICROARCH.md
+                                  HBM section: gfx950 FETCH_SIZE counts half of wide streaming reads)
+usage: tools/pmc_summary.py <tag> [gpurun_out/prof_<tag>]
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_kernel(path, counter):
+    vals = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] != counter or not row["Kernel_Name"].startswith("k_"):
+                continue
+            vals.setdefault(row["Kernel_Name"], []).append(float(row["Counter_Value"]))
+    return {k: statistics.median(v) for k, v in vals.items()}
+
+
+def main():
+    tag = sys.argv[1]
+    src = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    prof = os.path.join(ROOT, "profiles")
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    shutil.copy(os.path.join(src, "trace_serial", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats_serial.csv"))
+    for name in ("bench_under_trace.json", "bench_under_trace_serial.json"):
+        p = os.path.join(src, name)
+        if os.path.exists(p):
+            shutil.copy(p, os.path.join(prof, f"{tag}_{name}"))
+    fetch = per_kernel(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    out = {"_note": "HBM bytes per launch (median over launches) from rocprofv3 PMC, separate FETCH_SIZE / WRITE_SIZE "
+                    "passes of bench.py --steps 3 --inflight 1, corrected per MI355X_MICROARCH.md HBM section: "
+                    "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024; batch = 4096 std proofs; round " + tag}
+    for k in sorted(set(fetch) | set(write)):
+        f, w = fetch.get(k, 0.0), write.get(k, 0.0)
+        out[k] = int(round((2 * f + w) * 1024))
+        out[k + "_raw_KiB"] = {"FETCH_SIZE": f, "WRITE_SIZE": w}
+    json.dump(out, open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps({k: v for k, v in out.items() if not k.endswith("_KiB")}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Collect the round's profiles on the GPU box:
-#  1) kernel trace + stats of bench.py (timing source for profiles/)
-#  2) two separate PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic per kernel
+# Collect the round's profiles on the GPU box (then run tools/pmc_summary.py <tag> locally):
+#  1) kernel trace + stats of the default bench command (serial pass + two-in-flight pass)
+#  2) kernel trace + stats with --inflight 1: per-launch averages = bench's kernel_ms
+#  3) two separate PMC passes (FETCH_SIZE, WRITE_SIZE) for HBM traffic per kernel
 # usage: tools/profile_round.sh <tag>
 set -e
 TAG=${1:-r01}
@@ -10,6 +11,7 @@ cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/trace -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_under_trace.json 2> $OUT/trace.err
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_fetch.err
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_write.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/trace_serial -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --inflight 1 > $OUT/bench_under_trace_serial.json 2> $OUT/trace_serial.err
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --inflight 1 > /dev/null 2> $OUT/pmc_fetch.err
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --inflight 1 > /dev/null 2> $OUT/pmc_write.err
 echo done
