@@ -87,6 +87,16 @@ int  p2v_circuit_get_info(const p2v_circuit* c, p2v_circuit_info* info);
  * `error` or mis-verify on such input). */
 int  p2v_pack_proof_json(const p2v_circuit* c, const char* proof_json, size_t len, uint64_t* dst);
 
+/* Batch form of p2v_pack_proof_json, on `threads` host threads (<= 0: all cores): proof i
+ * goes to dst[i * proof_words], its code (P2V_OK / P2V_E_PARSE / P2V_E_SHAPE) to codes[i].
+ * Proofs whose JSON text equals the first proof's except for the numbers take a
+ * template-guided linear scan; any other proof goes through the full reader (same results,
+ * same errors).  Returns the number of proofs that failed (message of the first one in
+ * p2v_last_error_message), or a negative code on bad arguments.
+ * Replaces: `decode` of a list of ProofWithPublicInputs (Types.hs:245-254). */
+int  p2v_pack_proofs_json(const p2v_circuit* c, const char* const* jsons, const size_t* lens, size_t n,
+                          uint64_t* dst, int32_t* codes, int threads);
+
 /* ---- verification (GPU) ------------------------------------------------------------ */
 #define P2V_FLAG_INPUT_DEVICE  1u  /* `proofs` is a device pointer on the verifier's device  */
 #define P2V_FLAG_RESULT_DEVICE 2u  /* `results` (and trace) are device pointers              */

@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 #include "../../include/p2v.h"
 #include "circuit.hpp"
@@ -115,6 +116,52 @@ int p2v_pack_proof_json(const p2v_circuit* pc, const char* proof_json, size_t le
   } catch (const ShapeError& e) { return fail(P2V_E_SHAPE, e.what()); }
   catch (const ParseError& e) { return fail(P2V_E_PARSE, e.what()); }
   catch (const std::exception& e) { return fail(P2V_E_PARSE, e.what()); }
+}
+
+int p2v_pack_proofs_json(const p2v_circuit* pc, const char* const* jsons, const size_t* lens, size_t n, uint64_t* dst,
+                         int32_t* codes, int threads) {
+  if (!pc || (n && (!jsons || !lens || !dst || !codes))) return fail(P2V_E_ARG, "null argument");
+  if (n == 0) return 0;
+  const Circuit& C = pc->c;
+  const int64_t W = C.L.words;
+  auto dom_pack = [&](size_t i, std::string* msg) -> int32_t {
+    try {
+      JVal pj = parse_json(jsons[i], lens[i]);
+      pack_proof(C, pj, dst + (size_t)W * i);
+      return P2V_OK;
+    } catch (const ShapeError& e) { if (msg) *msg = e.what(); return P2V_E_SHAPE; }
+    catch (const ParseError& e) { if (msg) *msg = e.what(); return P2V_E_PARSE; }
+    catch (const std::exception& e) { if (msg) *msg = e.what(); return P2V_E_PARSE; }
+  };
+  // template from the first proof that packs
+  ProofTemplate T;
+  bool have_t = false;
+  size_t first = 0;
+  std::vector<std::string> msgs(n);
+  for (; first < n && !have_t; first++) {
+    try { have_t = T.build(C, jsons[first], lens[first], dst + (size_t)W * first); codes[first] = P2V_OK; }
+    catch (...) { codes[first] = dom_pack(first, &msgs[first]); }
+  }
+  auto work = [&](size_t a, size_t b) {
+    for (size_t i = a; i < b; i++) {
+      if (have_t && T.pack(jsons[i], lens[i], dst + (size_t)W * i)) { codes[i] = P2V_OK; continue; }
+      codes[i] = dom_pack(i, &msgs[i]);
+    }
+  };
+  const size_t rest = n - first;
+  int nt = threads > 0 ? threads : (int)std::thread::hardware_concurrency();
+  if (nt < 1) nt = 1;
+  if ((size_t)nt > rest) nt = (int)(rest ? rest : 1);
+  if (nt <= 1) work(first, n);
+  else {
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nt; t++) pool.emplace_back(work, first + rest * t / nt, first + rest * (t + 1) / nt);
+    for (auto& th : pool) th.join();
+  }
+  int nfail = 0;
+  for (size_t i = 0; i < n; i++)
+    if (codes[i] != P2V_OK) { if (!nfail) g_err = "proof " + std::to_string(i) + ": " + msgs[i]; nfail++; }
+  return nfail;
 }
 
 int p2v_device_count(void) {

@@ -293,10 +293,17 @@ namespace {
 struct Packer {
   const Circuit& C;
   uint64_t* dst;
+  int32_t* rec = nullptr;   // optional: packed word -> number ordinal (template recording)
+  void put(int64_t idx, const JVal& v) { dst[idx] = j_field(v); if (rec) rec[idx] = v.ord; }
+  void digest(const JVal& d, int64_t off) {   // Hash/Digest.hs:40-44
+    const auto& e = d.at("elements").arr();
+    if (e.size() != 4) throw ParseError("digest must have 4 elements");
+    for (int i = 0; i < 4; i++) put(off + i, e[i]);
+  }
   void fields(const JVal& v, int64_t off, int64_t n, const char* what) {
     const auto& a = v.arr();
     if ((int64_t)a.size() != n) throw ShapeError(std::string(what) + ": expected " + std::to_string(n) + " elements, got " + std::to_string(a.size()));
-    for (int64_t i = 0; i < n; i++) dst[off + i] = j_field(a[i]);
+    for (int64_t i = 0; i < n; i++) put(off + i, a[i]);
   }
   void exts(const JVal& v, int64_t off, int64_t n, const char* what) {
     const auto& a = v.arr();
@@ -304,20 +311,20 @@ struct Packer {
     for (int64_t i = 0; i < n; i++) {
       const auto& pr = a[i].arr();
       if (pr.size() != 2) throw ParseError("F^2 value must be a pair");
-      dst[off + 2 * i] = j_field(pr[0]); dst[off + 2 * i + 1] = j_field(pr[1]);
+      put(off + 2 * i, pr[0]); put(off + 2 * i + 1, pr[1]);
     }
   }
   void digests(const JVal& v, int64_t off, int64_t n, const char* what) {
     const auto& a = v.arr();
     if ((int64_t)a.size() != n) throw ShapeError(std::string(what) + ": expected " + std::to_string(n) + " digests, got " + std::to_string(a.size()));
-    for (int64_t i = 0; i < n; i++) digest_of(a[i], dst + off + 4 * i);
+    for (int64_t i = 0; i < n; i++) digest(a[i], off + 4 * i);
   }
 };
 }  // namespace
 
-void pack_proof(const Circuit& C, const JVal& root, uint64_t* dst) {
+void pack_proof(const Circuit& C, const JVal& root, uint64_t* dst, int32_t* rec) {
   const Layout& L = C.L;
-  Packer P{C, dst};
+  Packer P{C, dst, rec};
   const JVal& pr = root.at("proof");
   P.fields(root.at("public_inputs"), L.pis, C.num_pis, "public_inputs");
   P.digests(pr.at("wires_cap"), L.wcap, C.cap_len, "wires_cap");
@@ -339,7 +346,7 @@ void pack_proof(const Circuit& C, const JVal& root, uint64_t* dst) {
   if ((int)cc.size() != S) throw ShapeError("commit_phase_merkle_caps: expected " + std::to_string(S));
   for (int s = 0; s < S; s++) P.digests(cc[s], L.ccaps + (int64_t)s * 4 * C.cap_len, C.cap_len, "commit_phase_merkle_caps[s]");
   P.exts(fp.at("final_poly").at("coeffs"), L.final_poly, C.final_len, "final_poly.coeffs");
-  dst[L.pow] = j_field(fp.at("pow_witness"));
+  P.put(L.pow, fp.at("pow_witness"));
   const auto& qr = fp.at("query_round_proofs").arr();
   if ((int)qr.size() != C.num_queries) throw ShapeError("query_round_proofs: expected " + std::to_string(C.num_queries));
   for (int q = 0; q < C.num_queries; q++) {
@@ -359,6 +366,112 @@ void pack_proof(const Circuit& C, const JVal& root, uint64_t* dst) {
       P.digests(st[s].at("merkle_proof").at("siblings"), base + L.step_path[s], C.step_depth[s], "step siblings");
     }
   }
+}
+
+// ------------------------------------------------------------------ template-guided pack
+// Proofs of one circuit from one producer share their JSON text except for the numbers.
+// The template proof is parsed by the DOM reader recording every number token's span and
+// the packed word it lands in; a later proof whose bytes between number tokens equal the
+// template's has the same JSON tree, so its numbers go straight to those words.  Anything
+// else (other whitespace or key order, a non-integral token where a field element is
+// read) returns false and the caller uses the DOM reader, which also produces the
+// reference's error for malformed input.
+bool ProofTemplate::build(const Circuit& C, const char* s, size_t n, uint64_t* dst) {
+  spans.clear();
+  JVal root = JParser(s, n, &spans).parse();
+  std::vector<int32_t> rec((size_t)C.L.words, -1);
+  pack_proof(C, root, dst, rec.data());
+  dst_of.assign(spans.size(), -1);
+  for (int64_t w = 0; w < C.L.words; w++) if (rec[w] >= 0) dst_of[rec[w]] = w;
+  text.assign(s, n);
+  return true;
+}
+
+namespace {
+// 8 ASCII bytes (little-endian load) all in '0'..'9'?  Then their value (SWAR: three
+// multiplies instead of eight multiply-adds; the usual branch-free digit-block parse).
+inline bool eight_digits(uint64_t v) {
+  return (((v & 0xF0F0F0F0F0F0F0F0ULL) | (((v + 0x0606060606060606ULL) & 0xF0F0F0F0F0F0F0F0ULL) >> 4)) == 0x3333333333333333ULL);
+}
+inline uint32_t eight_value(uint64_t v) {
+  v -= 0x3030303030303030ULL;
+  v = v * 10 + (v >> 8);
+  v = (((v & 0x000000FF000000FFULL) * 0x000F424000000064ULL) + (((v >> 16) & 0x000000FF000000FFULL) * 0x0000271000000001ULL)) >> 32;
+  return (uint32_t)v;
+}
+inline uint64_t load8(const char* p) { uint64_t w; memcpy(&w, p, 8); return w; }
+// per byte of 8 ASCII bytes: 0x80 where the byte is not '0'..'9' (bytes >= 0x80: caller checks)
+inline uint64_t nondigit_mask(uint64_t v) {
+  const uint64_t a = (v & 0xF0F0F0F0F0F0F0F0ULL) ^ 0x3030303030303030ULL;
+  const uint64_t b = ((v + 0x0606060606060606ULL) & 0xF0F0F0F0F0F0F0F0ULL) ^ 0x3030303030303030ULL;
+  const uint64_t m = a | b;
+  return (((m & 0x7F7F7F7F7F7F7F7FULL) + 0x7F7F7F7F7F7F7F7FULL) | m) & 0x8080808080808080ULL;
+}
+// integer token starting at s (optional '-', then digits) -> its end and its field value;
+// false if the token continues with a fraction / exponent character (caller falls back)
+inline bool number_fast(const char* s, const char* end, const char*& tok_end, uint64_t& out) {
+  const char* p = s;
+  const bool neg = *p == '-';
+  p += neg;
+  const char* q = p;
+  for (;;) {   // digit run
+    if (q + 8 <= end) {
+      const uint64_t v = load8(q);
+      if (v & 0x8080808080808080ULL) { while (q < end && *q >= '0' && *q <= '9') q++; break; }
+      const uint64_t m = nondigit_mask(v);
+      if (m) { q += __builtin_ctzll(m) >> 3; break; }
+      q += 8;
+    } else { while (q < end && *q >= '0' && *q <= '9') q++; break; }
+  }
+  tok_end = q;
+  if (q < end && is_num_char(*q)) return false;   // '.', 'e', 'E', '+', '-' inside the token
+  const size_t nd = (size_t)(q - p);
+  if (nd == 0) return false;
+  uint64_t acc;
+  if (nd > 20) {
+    if (!field_of_text(s, (size_t)(q - s), out)) return false;
+    return true;
+  }
+  acc = 0;
+  size_t i = 0;
+  const size_t head = nd > 19 ? 19 : nd;
+  for (; i + 8 <= head; i += 8) acc = acc * 100000000ULL + eight_value(load8(p + i));
+  for (; i < head; i++) acc = acc * 10 + (uint64_t)(p[i] - '0');
+  if (nd == 20) {   // acc < 10^19: acc*10 + d < 2^64 * 10 -> fold 2^64 == 2^32 - 1 (mod p)
+    const unsigned __int128 x = (unsigned __int128)acc * 10 + (uint64_t)(p[19] - '0');
+    const uint64_t hi = (uint64_t)(x >> 64), lo = (uint64_t)x;
+    uint64_t r = lo + hi * 0xFFFFFFFFULL;
+    if (r < lo) r += 0xFFFFFFFFULL;
+    acc = r;
+  }
+  while (acc >= GL_P) acc -= GL_P;
+  out = (neg && acc) ? GL_P - acc : acc;
+  return true;
+}
+inline bool same(const char* a, const char* b, size_t n) {
+  if (n <= 16) { for (size_t i = 0; i < n; i++) if (a[i] != b[i]) return false; return true; }
+  return memcmp(a, b, n) == 0;
+}
+}  // namespace
+
+bool ProofTemplate::pack(const char* s, size_t n, uint64_t* dst) const {
+  const char* t = text.data();
+  size_t ps = 0, pt = 0;
+  for (size_t k = 0; k < spans.size(); k++) {
+    const size_t seg = spans[k].first - pt;   // skeleton bytes before number k
+    if (ps + seg > n || !same(s + ps, t + pt, seg)) return false;
+    ps += seg;
+    pt = spans[k].second;
+    if (ps >= n || !(s[ps] == '-' || (s[ps] >= '0' && s[ps] <= '9'))) return false;
+    const char* te;
+    uint64_t val;
+    if (!number_fast(s + ps, s + n, te, val)) return false;
+    ps = (size_t)(te - s);
+    const int64_t w = dst_of[k];
+    if (w >= 0) dst[w] = val;
+  }
+  const size_t tail = text.size() - pt;
+  return ps + tail == n && memcmp(s + ps, t + pt, tail) == 0;
 }
 
 }  // namespace p2v

@@ -68,7 +68,17 @@ struct Circuit {
 };
 
 Circuit parse_circuit(const JVal& common, const JVal& vkey);   // throws ParseError / CircuitError
-void pack_proof(const Circuit& c, const JVal& proof, uint64_t* dst);   // throws ParseError / ShapeError
+// throws ParseError / ShapeError; rec (optional, [words]) receives each packed word's number ordinal
+void pack_proof(const Circuit& c, const JVal& proof, uint64_t* dst, int32_t* rec = nullptr);
+
+// template-guided fast path of pack_proof (circuit.cpp); pack() == false: use pack_proof
+struct ProofTemplate {
+  std::string text;
+  std::vector<std::pair<size_t, size_t>> spans;   // number tokens of the template text
+  std::vector<int64_t> dst_of;                    // number ordinal -> packed word (-1: unused)
+  bool build(const Circuit& c, const char* s, size_t n, uint64_t* dst);   // throws like pack_proof
+  bool pack(const char* s, size_t n, uint64_t* dst) const;
+};
 GateDesc parse_gate_string(const std::string& s);              // Gate/Parser.hs:107-130
 
 }  // namespace p2v

@@ -15,12 +15,16 @@ struct ParseError : std::runtime_error { using std::runtime_error::runtime_error
 struct ShapeError : std::runtime_error { using std::runtime_error::runtime_error; };
 struct CircuitError : std::runtime_error { using std::runtime_error::runtime_error; };
 
+// characters of a number token (the reader is permissive; typed accessors validate)
+inline bool is_num_char(char c) { return (c >= '0' && c <= '9') || c == '.' || c == 'e' || c == 'E' || c == '+' || c == '-'; }
+
 struct JVal {
   enum Kind { Null, Bool, Num, Str, Arr, Obj } kind = Null;
   bool b = false;
   std::string text;                    // number text / string value
   std::vector<JVal> items;             // array items / object values
   std::vector<std::string> keys;       // object keys
+  int32_t ord = -1;                    // number: ordinal in document order
 
   const JVal* get(const char* k) const {
     if (kind != Obj) return nullptr;
@@ -40,7 +44,7 @@ struct JVal {
 
 class JParser {
  public:
-  JParser(const char* s, size_t n) : s_(s), n_(n) {}
+  JParser(const char* s, size_t n, std::vector<std::pair<size_t, size_t>>* spans = nullptr) : s_(s), n_(n), spans_(spans) {}
   JVal parse() {
     JVal v; value(v); ws();
     if (i_ != n_) throw ParseError("trailing characters after JSON value");
@@ -48,6 +52,8 @@ class JParser {
   }
  private:
   const char* s_; size_t n_, i_ = 0;
+  std::vector<std::pair<size_t, size_t>>* spans_;   // number token [start, end) by ordinal
+  int32_t nnum_ = 0;
   void ws() { while (i_ < n_ && (s_[i_] == ' ' || s_[i_] == '\n' || s_[i_] == '\r' || s_[i_] == '\t')) i_++; }
   [[noreturn]] void bad(const char* m) { throw ParseError(std::string("JSON syntax: ") + m + " at offset " + std::to_string(i_)); }
   void str(std::string& out) {
@@ -102,8 +108,10 @@ class JParser {
     if (!strncmp(s_ + i_, "null", 4) && i_ + 4 <= n_) { v.kind = JVal::Null; i_ += 4; return; }
     if (c == '-' || (c >= '0' && c <= '9')) {
       size_t st = i_++;
-      while (i_ < n_ && (isdigit((unsigned char)s_[i_]) || s_[i_] == '.' || s_[i_] == 'e' || s_[i_] == 'E' || s_[i_] == '+' || s_[i_] == '-')) i_++;
-      v.kind = JVal::Num; v.text.assign(s_ + st, i_ - st); return;
+      while (i_ < n_ && is_num_char(s_[i_])) i_++;
+      v.kind = JVal::Num; v.text.assign(s_ + st, i_ - st); v.ord = nnum_++;
+      if (spans_) spans_->emplace_back(st, i_);
+      return;
     }
     bad("unexpected character");
   }
@@ -114,21 +122,30 @@ inline JVal parse_json(const char* s, size_t n) { return JParser(s, n).parse(); 
 // ---- typed accessors ---------------------------------------------------------------
 static constexpr uint64_t GL_P = 0xFFFFFFFF00000001ULL;
 
-// aeson Integer -> mod p (negative numbers reduce to the non-negative residue)
+// aeson Integer -> mod p (negative numbers reduce to the non-negative residue).
+// Number token text [s, s+n) -> false if it is not an integer.
+inline bool field_of_text(const char* s, size_t n, uint64_t& out) {
+  size_t i = 0; bool neg = false;
+  if (n && s[0] == '-') { neg = true; i = 1; }
+  if (i >= n) return false;
+  uint64_t acc = 0;
+  // up to 19 digits accumulate exactly in 64 bits; longer integers reduce as they go
+  for (; i < n; i++) {
+    const unsigned d = (unsigned)(s[i] - '0');
+    if (d > 9) return false;
+    if (acc < 1000000000000000000ULL) acc = acc * 10 + d;
+    else acc = (uint64_t)(((unsigned __int128)acc * 10 + d) % GL_P);
+  }
+  if (acc >= GL_P) acc -= GL_P;
+  out = (neg && acc) ? GL_P - acc : acc;
+  return true;
+}
 inline uint64_t j_field(const JVal& v) {
   if (v.kind != JVal::Num) throw ParseError("expected an integer field element");
-  const std::string& t = v.text;
-  size_t i = 0; bool neg = false;
-  if (!t.empty() && t[0] == '-') { neg = true; i = 1; }
-  if (i >= t.size()) throw ParseError("bad number");
-  unsigned __int128 acc = 0;
-  for (; i < t.size(); i++) {
-    char c = t[i];
-    if (c < '0' || c > '9') throw ParseError("non-integral number where a field element is expected");
-    acc = (acc * 10 + (unsigned)(c - '0')) % GL_P;
-  }
-  uint64_t r = (uint64_t)acc;
-  return (neg && r) ? GL_P - r : r;
+  uint64_t r;
+  if (v.text.empty() || (v.text[0] == '-' && v.text.size() == 1)) throw ParseError("bad number");
+  if (!field_of_text(v.text.data(), v.text.size(), r)) throw ParseError("non-integral number where a field element is expected");
+  return r;
 }
 inline int64_t j_int(const JVal& v) {
   if (v.kind != JVal::Num) throw ParseError("expected an integer");

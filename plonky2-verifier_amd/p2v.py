@@ -105,6 +105,7 @@ def lib() -> ctypes.CDLL:
     L.p2v_circuit_free.restype = None
     L.p2v_circuit_get_info.argtypes = [vp, ctypes.POINTER(_Info)]
     L.p2v_pack_proof_json.argtypes = [vp, ctypes.c_char_p, sz, u64p]
+    L.p2v_pack_proofs_json.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz, u64p, vp, ctypes.c_int]
     L.p2v_device_count.argtypes = []
     L.p2v_verifier_create.argtypes = [vp, ctypes.c_int, sz, ctypes.POINTER(vp)]
     L.p2v_verifier_free.argtypes = [vp]
@@ -183,10 +184,24 @@ class VerifierCircuitData:
         _check(lib().p2v_pack_proof_json(self._h, b, len(b), out.ctypes.data))
         return out
 
-    def pack_many(self, proofs: Sequence[Union[str, bytes]]) -> np.ndarray:
-        arr = np.empty((len(proofs), self.info.proof_words), dtype=np.uint64)
-        for i, p in enumerate(proofs):
-            self.pack(p, arr[i])
+    def pack_many(self, proofs: Sequence[Union[str, bytes]], threads: int = 0, codes: Optional[np.ndarray] = None) -> np.ndarray:
+        """A list of ProofWithPublicInputs JSON texts -> [n, proof_words] packed words, on
+        `threads` host threads (0: all cores; p2v_pack_proofs_json).  Raises P2VError for the
+        first proof that does not decode unless `codes` (int32 [n]) is given to receive the
+        per-proof codes (rows of failed proofs are then undefined)."""
+        bs = [_bytes(p) for p in proofs]
+        n = len(bs)
+        arr = np.empty((n, self.info.proof_words), dtype=np.uint64)
+        if n == 0:
+            return arr
+        ptrs = (ctypes.c_char_p * n)(*bs)
+        lens = (ctypes.c_size_t * n)(*[len(b) for b in bs])
+        cd = np.empty(n, dtype=np.int32) if codes is None else codes
+        assert cd.dtype == np.int32 and cd.size == n
+        nfail = lib().p2v_pack_proofs_json(self._h, ptrs, lens, n, arr.ctypes.data, cd.ctypes.data, threads)
+        if nfail < 0 or (nfail > 0 and codes is None):
+            bad = int(np.flatnonzero(cd != E_OK)[0]) if nfail > 0 else 0
+            raise P2VError(int(cd[bad]) if nfail > 0 else nfail, lib().p2v_last_error_message().decode(errors="replace"))
         return arr
 
     def __del__(self):

@@ -77,6 +77,40 @@ def test_pack_shape_and_parse_errors(edit, code):
     assert e.value.code == -1
 
 
+def test_batch_pack_template_path_matches_dom_reader():
+    """p2v_pack_proofs_json: the template-guided scan gives the DOM reader's words on
+    every proof, and every other text (whitespace, key order, exotic numbers, malformed)
+    falls back to the DOM reader with its exact result or error code."""
+    p2v = p2v_module()
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    proofs = [gc.proof(1 + i % 2, 40 + i) for i in range(6)]
+    pw = json.loads(proofs[3])["proof"]["opening_proof"]["pow_witness"]
+    key = b'"pow_witness":%d' % pw
+    assert key in proofs[3]
+    numbers = [b"-%d" % pw, b"%d" % (pw + 3 * P), b"%d" % P, b"%d" % (P - 1), b"-0", b"0000000000000000000000012",
+               b"9999999999999999999", b"-9999999999999999999", b"18446744073709551615", b"99999999999999999999",
+               b"100000000000000000000", b"12345678", b"1e5", b"12.0", b"-", b"1-2"]
+    variants = [proofs[3].replace(key, b'"pow_witness":' + v) for v in numbers]
+    variants += [json.dumps(json.loads(proofs[4]), indent=1).encode(),                     # other whitespace
+                 json.dumps(dict(reversed(list(json.loads(proofs[5]).items())))).encode(),  # other key order
+                 proofs[2][:-7], b"[]"]                                                    # malformed
+    batch = proofs + variants
+    codes = np.empty(len(batch), np.int32)
+    got = vk.pack_many(batch, threads=3, codes=codes)
+    for i, text in enumerate(batch):
+        try:
+            want, code = vk.pack(text), 0
+        except p2v.P2VError as e:
+            want, code = None, e.code
+        assert codes[i] == code, (i, text[-40:])
+        if code == 0:
+            assert np.array_equal(got[i], want), i
+    assert (codes != 0).sum() == 6   # 1e5, 12.0, "-", 1-2, truncated, []
+    with pytest.raises(p2v.P2VError):
+        vk.pack_many([proofs[0], proofs[1][:-3]])
+
+
 def _common_edit(fn):
     gc = gen_circuit(6, 4, 0)
     d = json.loads(gc.common)
