@@ -82,14 +82,17 @@ __device__ __forceinline__ uint32_t add_co(uint32_t a, uint32_t b, uint64_t& co)
 __device__ __forceinline__ uint32_t addc_co(uint32_t a, uint32_t b, uint64_t ci, uint64_t& co) { uint32_t d; asm("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(a), "v"(b), "s"(ci)); return d; }
 __device__ __forceinline__ uint32_t addc0(uint32_t a, uint64_t ci) { uint32_t d; uint64_t co; asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(d), "=s"(co) : "v"(a), "s"(ci)); return d; }
 __device__ __forceinline__ uint32_t sub_co(uint32_t a, uint32_t b, uint64_t& co) { uint32_t d; asm("v_sub_co_u32_e64 %0, %1, %2, %3" : "=v"(d), "=s"(co) : "v"(a), "v"(b)); return d; }
+__device__ __forceinline__ uint32_t subb_co(uint32_t a, uint32_t b, uint64_t ci, uint64_t& co) { uint32_t d; asm("v_subb_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(a), "v"(b), "s"(ci)); return d; }
 __device__ __forceinline__ uint32_t subb0_co(uint32_t a, uint64_t ci, uint64_t& co) { uint32_t d; asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(d), "=s"(co) : "v"(a), "s"(ci)); return d; }
 __device__ __forceinline__ uint32_t mask_m1(uint64_t m) { uint32_t d; asm("v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(d) : "s"(m)); return d; }
 __device__ __forceinline__ uint32_t mask_1(uint64_t m) { uint32_t d; asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(d) : "s"(m)); return d; }
 }  // namespace ax
 
 // a * b (mod p) for any a, b < 2^64, result in [0, 2^64) (not necessarily canonical).
-// 17 VALU: 4 partial products, the exact 128-bit product through the carry chain, then
-// lo + hi_lo (2^32 - 1) - hi_hi with one fix-up per wrap (2^64 == 2^32 - 1 mod p).
+// 16 VALU: 4 partial products; the 128-bit product lo + h0 2^64 + h1 2^96 through the
+// carry chain, where the carry cm of the middle sum a0 b1 + a1 b0 (weight 2^96) is not
+// added into h1 but enters the subtraction of h1 as its borrow-in; then
+// lo + h0 (2^32 - 1) - h1 (2^64 == 2^32 - 1, 2^96 == -1 mod p) with one fix-up per wrap.
 __device__ __forceinline__ uint64_t mul_nc_dev(uint64_t a, uint64_t b) {
   using namespace ax;
   const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
@@ -100,12 +103,12 @@ __device__ __forceinline__ uint64_t mul_nc_dev(uint64_t a, uint64_t b) {
   const uint64_t p11 = mad0(a1, b1);
   const uint32_t lo1 = add_co((uint32_t)(p00 >> 32), (uint32_t)m, c1);
   const uint32_t h0 = addc_co((uint32_t)p11, (uint32_t)(m >> 32), c1, c2);
-  const uint32_t h1 = addc0((uint32_t)(p11 >> 32), c2) + mask_1(cm);   // exact: the product is < 2^128
+  const uint32_t h1 = addc0((uint32_t)(p11 >> 32), c2);                 // + cm: below
   const uint64_t lo = ((uint64_t)lo1 << 32) | (uint32_t)p00;
   const uint64_t t = madm1_co(h0, lo, ct);                              // lo + h0 (2^32 - 1)
   const uint32_t tl = add_co((uint32_t)t, mask_m1(ct), c4);             // wrapped: + 2^32 - 1
   const uint32_t th = addc0((uint32_t)(t >> 32), c4);
-  const uint32_t rl = sub_co(tl, h1, bw1);                              // - h1
+  const uint32_t rl = subb_co(tl, h1, cm, bw1);                         // - (h1 + cm) < 2^32
   const uint32_t rh = subb0_co(th, bw1, bw2);
   const uint32_t rl2 = sub_co(rl, mask_m1(bw2), bw3);                   // wrapped: - (2^32 - 1)
   const uint32_t rh2 = subb0_co(rh, bw3, bw4);

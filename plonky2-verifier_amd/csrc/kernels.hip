@@ -58,7 +58,11 @@ __device__ __forceinline__ void leaf_hash_unit(const DevCircuit& c, int unit, in
     const int k = len - i;
 #pragma unroll
     for (int j = 0; j < 8; j++) if (j < k) st[j] = ld(c, off + i + j, p);
-    p2::permute(st);
+    // words the rest of the sponge reads: the digest (0..3) after the last block, else the
+    // words the next block does not overwrite (nx.. 11); state words 8..11 are 0 in block 0
+    const int nx = k - 8;
+    const int gm = nx <= 0 ? 1 : (nx >= 8 ? 4 : ((7 << (nx >> 2)) & 7));
+    p2::permute_dev(st, i == 0, gm);
   }
   uint64_t* dst = c.leafdig + ((int64_t)(q * c.T + t) * 4) * c.B + p;
 #pragma unroll
@@ -305,7 +309,7 @@ extern "C" __global__ void __launch_bounds__(256) k_merkle(DevCircuit c) {
     uint64_t st[12];
 #pragma unroll
     for (int i = 0; i < 4; i++) { st[i] = odd ? sib[i] : cur[i]; st[4 + i] = odd ? cur[i] : sib[i]; st[8 + i] = 0; }
-    p2::permute(st);
+    p2::permute_dev(st, true, 1);   // compress: words 8..11 enter as 0, only 0..3 are read
 #pragma unroll
     for (int i = 0; i < 4; i++) cur[i] = st[i];
     idx >>= 1;

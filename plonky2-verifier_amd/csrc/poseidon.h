@@ -108,16 +108,172 @@ __host__ __device__ __forceinline__ void partial_round(uint64_t s[12], int r) {
   mds(s);
 }
 
+#if defined(__HIPCC__)
+// ---------------------------------------------------------------- device permutation
+// Same function, restructured for the gfx950 VALU (one permutation per lane):
+//  * the round constant of round r+1 is folded into round r's MDS: each row's two 32-bit-half
+//    accumulators START at the constant's halves (the first v_mad_u64_u32's addend), so
+//    rounds 1..29 spend no instruction on constant addition;
+//  * every MDS multiply-add is an explicit v_mad_u64_u32 with the matrix entry as an inline
+//    constant (the compiler otherwise turns 2/16 into 64-bit shifts of zero-extended register
+//    pairs and pays a v_mov per pair);
+//  * rounds alternate between two register sets (s -> t -> s), so no copies are needed at
+//    loop edges; full rounds run as 4 pairs, partial rounds as 11 pairs.
+struct RcSplit { uint64_t lo[31 * 12], hi[31 * 12]; };   // round 30 = 0 (after the last MDS)
+__host__ __device__ constexpr RcSplit make_rc_split() {
+  RcSplit t{};
+  constexpr uint64_t rc[360] = P2V_ALL_ROUND_CONSTANTS_INIT;
+  for (int k = 0; k < 360; k++) { t.lo[k] = rc[k] & 0xFFFFFFFFull; t.hi[k] = rc[k] >> 32; }
+  return t;
+}
+// S-box outputs of round 0 for state words 8..11 when they enter as 0 (2-to-1 compression
+// and the first block of every sponge): sbox(rc[0][8 + i]).
+struct ZhConst { uint64_t z[4]; };
+__host__ __device__ constexpr uint64_t cx_mul(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) % gl::P); }
+__host__ __device__ constexpr ZhConst make_zh() {
+  ZhConst t{};
+  constexpr uint64_t rc[360] = P2V_ALL_ROUND_CONSTANTS_INIT;
+  for (int i = 0; i < 4; i++) {
+    const uint64_t x = rc[8 + i] % gl::P, x2 = cx_mul(x, x), x3 = cx_mul(x2, x), x4 = cx_mul(x2, x2);
+    t.z[i] = cx_mul(x3, x4);
+  }
+  return t;
+}
+static __constant__ RcSplit c_rc_split = make_rc_split();
+static __constant__ ZhConst c_zh = make_zh();
+#endif
+
+#if defined(__HIP_DEVICE_COMPILE__)
+namespace dv {
+// acc + C a as one v_mad_u64_u32 with the matrix entry C as an inline constant.  The carry-out
+// is never needed: it goes to a fixed, clobbered SGPR pair rather than an asm output (an asm
+// SGPR output costs a wait state before every consumer, and the compiler would turn C = 2, 16
+// into 64-bit shifts of zero-extended register pairs).
+template <uint32_t C>
+__device__ __forceinline__ uint64_t madk(uint32_t a, uint64_t acc) {
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, s[94:95], %1, %2, %3" : "=v"(d) : "v"(a), "n"(C), "v"(acc) : "s94", "s95");
+  return d;
+}
+template <uint32_t C>
+__device__ __forceinline__ uint64_t madk_s(uint32_t a, uint64_t acc) {   // acc wave-uniform (SGPR pair)
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, s[94:95], %1, %2, %3" : "=v"(d) : "v"(a), "n"(C), "s"(acc) : "s94", "s95");
+  return d;
+}
+// al + 2^32 ah (al, ah < 2^43) -> [0, 2^64), congruent mod p: t = al + ah_hi (2^32 - 1), then
+// + ah_lo 2^32 on the high word; a carry out (2^64 == 2^32 - 1) adds 2^32 - 1 back.  5 VALU.
+__device__ __forceinline__ uint64_t reduce_rows(uint64_t al, uint64_t ah) {
+  using namespace gl::ax;
+  uint64_t c1, c2;
+  const uint64_t t = madm1_co((uint32_t)(ah >> 32), al, c1);   // < 2^44: no carry
+  const uint32_t rh = add_co((uint32_t)(t >> 32), (uint32_t)ah, c1);
+  const uint32_t rl = add_co((uint32_t)t, mask_m1(c1), c2);
+  return ((uint64_t)addc0(rh, c2) << 32) | rl;
+}
+template <int I, int J>
+__device__ __forceinline__ void mds_acc(const uint64_t* s, uint64_t& al, uint64_t& ah) {
+  if constexpr (J < 12) {
+    constexpr uint32_t C = mds_coeff(I, J);
+    al = madk<C>((uint32_t)s[J], al);
+    ah = madk<C>((uint32_t)(s[J] >> 32), ah);
+    mds_acc<I, J + 1>(s, al, ah);
+  }
+}
+// t[I..E) = (M s)[I..E) + k (k = the next round's constants, split into halves)
+template <int I, int E>
+__device__ __forceinline__ void mds_rows(const uint64_t* s, uint64_t* t, const uint64_t* kl, const uint64_t* kh) {
+  if constexpr (I < E) {
+    constexpr uint32_t C = mds_coeff(I, 0);
+    uint64_t al = madk_s<C>((uint32_t)s[0], kl[I]);
+    uint64_t ah = madk_s<C>((uint32_t)(s[0] >> 32), kh[I]);
+    mds_acc<I, 1>(s, al, ah);
+    t[I] = reduce_rows(al, ah);
+    mds_rows<I + 1, E>(s, t, kl, kh);
+  }
+}
+// round r: s -> t (s is clobbered by the S-boxes); t = M sbox(s) + rc[r + 1].
+// zh0: round 0 with state words 8..11 entering as 0 (their S-box outputs are constants).
+// g: which groups of 4 output rows are needed (bit k = rows 4k..4k+3); wave-uniform.
+template <bool FULL>
+__device__ __forceinline__ void round_pp(uint64_t* s, uint64_t* t, int r, bool zh0, int g) {
+  if (FULL) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = sbox(s[i]);
+    if (zh0) {
+#pragma unroll
+      for (int i = 8; i < 12; i++) s[i] = c_zh.z[i - 8];
+    } else {
+#pragma unroll
+      for (int i = 8; i < 12; i++) s[i] = sbox(s[i]);
+    }
+  } else {
+    s[0] = sbox(s[0]);
+  }
+  const uint64_t* kl = c_rc_split.lo + 12 * (r + 1);
+  const uint64_t* kh = c_rc_split.hi + 12 * (r + 1);
+  if (g & 1) mds_rows<0, 4>(s, t, kl, kh);
+  if (g & 2) mds_rows<4, 8>(s, t, kl, kh);
+  if (g & 4) mds_rows<8, 12>(s, t, kl, kh);
+}
+}  // namespace dv
+
+// Device permutation, one per lane.  zh: state words 8..11 are 0 on entry (2-to-1 compression,
+// first sponge block).  gm: groups of 4 output words the caller reads (bit k = words
+// 4k..4k+3); the others are left undefined.  Both wave-uniform.  Same function as
+// Hash/Poseidon.hs:42-101, restructured for the gfx950 VALU:
+//  * the round constant of round r+1 is folded into round r's MDS: each row's two 32-bit-half
+//    accumulators START at the constant's halves (the first v_mad_u64_u32's addend), so
+//    rounds 1..29 spend no instruction on constant addition;
+//  * every MDS multiply-add is an explicit v_mad_u64_u32 with the matrix entry as an inline
+//    constant;
+//  * rounds alternate between two register sets (s -> t -> s), so no copies are needed at
+//    loop edges; full rounds run as 4 pairs, partial rounds as 11 pairs.
+__device__ __forceinline__ void permute_dev(uint64_t s[12], bool zh = false, int gm = 7) {
+  uint64_t t[12];
+  // keep zh / gm run-time uniform values (uniform branches); as compile-time constants the
+  // compiler peels loop iterations and the extra code raises register pressure
+  int fl = __builtin_amdgcn_readfirstlane((zh ? 8 : 0) | gm);
+  asm("" : "+s"(fl));
+  zh = fl & 8;
+  gm = fl & 7;
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = add_nc(s[i], c_round_constants[i]);
+  if (!zh) {
+#pragma unroll
+    for (int i = 8; i < 12; i++) s[i] = add_nc(s[i], c_round_constants[i]);
+  }
+#pragma unroll 1
+  for (int k = 0; k < 4; k++) {   // full-round pairs (0,1) (2,3) (26,27) (28,29)
+    const int r = k < 2 ? 2 * k : 22 + 2 * k;
+    dv::round_pp<true>(s, t, r, zh && k == 0, 7);
+    dv::round_pp<true>(t, s, r + 1, false, k == 3 ? gm : 7);
+    if (k == 1) {
+#pragma unroll 1
+      for (int q = 4; q < 26; q += 2) {   // partial-round pairs
+        dv::round_pp<false>(s, t, q, false, 7);
+        dv::round_pp<false>(t, s, q + 1, false, 7);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 12; i++) s[i] = gl::canon(s[i]);
+}
+#elif defined(__HIPCC__)
+__device__ void permute_dev(uint64_t s[12], bool zh = false, int gm = 7);   // device-only
+#endif
+
 // Hash/Poseidon.hs:42-46.  Inputs may be any value < 2^64; outputs are canonical.
 __host__ __device__ __forceinline__ void permute(uint64_t s[12]) {
-#pragma unroll 1
+#if defined(__HIP_DEVICE_COMPILE__)
+  permute_dev(s);
+#else
   for (int r = 0; r < 4; r++) full_round(s, r);
-#pragma unroll 1
   for (int r = 4; r < 26; r++) partial_round(s, r);
-#pragma unroll 1
   for (int r = 26; r < 30; r++) full_round(s, r);
   P2_UNROLL
   for (int i = 0; i < 12; i++) s[i] = gl::canon(s[i]);
+#endif
 }
 
 }  // namespace p2
