@@ -40,10 +40,10 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_workload(degree_bits, distinct, witnesses, seed_base, threads):
+def make_workload(degree_bits, distinct, witnesses, seed_base, threads, lookups=0):
     from support import generator
     g = generator()
-    gc = g.circuit(degree_bits, 4, 0, 1, 28, 16)
+    gc = g.circuit(degree_bits, 4, lookups, 1, 28, 16)
     wseeds = [seed_base * 1000 + i + 1 for i in range(witnesses)]
     with cf.ThreadPoolExecutor(threads) as ex:
         list(ex.map(gc.witness, wseeds))
@@ -161,7 +161,10 @@ def main():
     ap.add_argument("--witnesses", type=int, default=8)
     ap.add_argument("--degree-bits", type=int, default=12)
     ap.add_argument("--inflight", type=int, default=2, help="batches in flight per GPU (workspaces/streams)")
+    ap.add_argument("--lookups", type=int, default=0,
+                    help="0: standard recursion circuit (C2); 2: + LookupGate/LookupTableGate with a 256-entry and a 2^16-entry table (C3 circuit)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--quick", action="store_true", help="device-resident figure only (no ingest / PCIe / CPU legs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -176,7 +179,7 @@ def main():
 
     threads = max(1, min(16, (os.cpu_count() or 8)))
     t0 = time.time()
-    gc, proofs = make_workload(args.degree_bits, args.distinct, args.witnesses, rank + 1, threads)
+    gc, proofs = make_workload(args.degree_bits, args.distinct, args.witnesses, rank + 1, threads, args.lookups)
     log(f"[rank {rank}] generated {len(proofs)} distinct proofs in {time.time() - t0:.1f}s")
     vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
     info = vk.info
@@ -252,8 +255,9 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "proofs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u64 (Goldilocks mod-p integer)", "data": "synthetic",
-            "config": {"workload": f"C2: {B} std-config Plonky2 proofs per GPU per step (degree_bits {info.degree_bits}, "
-                                   f"28 FRI queries, arity 16, deg-2 ext), {len(proofs)} distinct tiled, device-resident",
+            "config": {"workload": f"{'C3' if args.lookups else 'C2'}: {B} std-config Plonky2 proofs per GPU per step (degree_bits {info.degree_bits}, "
+                                   f"28 FRI queries, arity 16, deg-2 ext{', lookups: 256 + 65536-entry tables' if args.lookups > 1 else (', lookups' if args.lookups else '')}), "
+                                   f"{len(proofs)} distinct tiled, device-resident",
                        "global_batch": B * world, "degree_bits": info.degree_bits, "parallelism": f"proof-sharded x{world}",
                        "inflight": nv},
             "serial": {"value": round(total / dt_serial, 1), "ms_per_step": round(dt_serial / args.steps * 1e3, 4),
@@ -266,10 +270,10 @@ def main():
             "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
             "verified_all": ok,
         }
-        if world == 1:
+        if world == 1 and not args.quick:
             out["ingest"] = ingest_rate(vk, proofs, threads)
             out["h2d_end_to_end"] = h2d_rate(bvs[0], tiled, B)
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not args.quick:
             out["cpu_baseline"] = cpu_baseline(gc, proofs, threads)
         print(json.dumps(out), flush=True)
     if world > 1:

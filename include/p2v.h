@@ -143,8 +143,10 @@ const char* p2v_version(void);
  *   off_q_folded     2Q   value after the last folding step Plonk/FRI.hs:306-323
  *   off_q_final      2Q   final polynomial at x_final       Plonk/FRI.hs:325-327
  *   off_flags        1    bit0 eqs_ok, bit1 pow_ok
- * total = 4 + 3r + 4r + 4 + 2S + 1 + Q + 4r + 6Q + 1
+ *   off_lut_re       rL   evalFinalRE of table k in challenge round i at [i*L + k]
+ *                         (L = #luts)                       Plonk/Lookups.hs:103-109
+ * total = 4 + 3r + 4r + 4 + 2S + 1 + Q + 4r + 6Q + 1 + rL
  */
-#define P2V_TRACE_WORDS(r, S, Q) (4 + 3*(r) + 4*(r) + 4 + 2*(S) + 1 + (Q) + 4*(r) + 6*(Q) + 1)
+#define P2V_TRACE_WORDS(r, S, Q, L) (4 + 3*(r) + 4*(r) + 4 + 2*(S) + 1 + (Q) + 4*(r) + 6*(Q) + 1 + (r)*(L))
 
 #endif /* P2V_H */

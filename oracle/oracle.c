@@ -593,7 +593,7 @@ static E eval_gate_selector_poly(const circuit_t* C, E x, int k) {
  * over F^2 — the straight-line program of Gate/Computation.hs:117-164 only names
  * intermediate values, so direct evaluation gives the same field elements. */
 typedef struct { const E* sel; int nsel; const E* lsel; int nlsel; const E* konst; int nkonst; const E* wires; int nwires; const F* pih; } evars_t;
-typedef struct { E* v; int n, cap; arena* m; } clist;
+typedef struct { E* v; int n, cap; arena* m; F* lutre; } clist;   /* lutre: evalFinalRE values for the trace */
 static void cpush(clist* l, E x) {
   if (l->n == l->cap) { int nc = l->cap ? 2 * l->cap : 64; E* nv = (E*)aalloc(l->m, nc * sizeof(E)); if (l->n) memcpy(nv, l->v, l->n * sizeof(E)); l->v = nv; l->cap = nc; }
   l->v[l->n++] = x;
@@ -845,6 +845,7 @@ static void eval_lookup_equations(const circuit_t* C, const constcols_t* cc, con
         F x = fadd(C->lut_in[k][j], fmul(D->B, C->lut_out[k][j]));
         cur = fadd(fmul(D->delta, cur), x);
       }
+      if (out->lutre) out->lutre[rr * C->nluts + k] = cur;
       cpush(out, Emul(SEL(4 + k), Esub(re, Eb(cur))));
     }
     {   /* eq_re_trans */
@@ -1100,7 +1101,7 @@ __attribute__((noinline)) static int verify_body(const circuit_t* C, const proof
        o_pw = o_fb + 2 * nsteps, o_qi = o_pw + 1, o_c = o_qi + Q, o_q = o_c + 2 * r, o_qin = o_q + 2 * r, o_qf = o_qin + 2 * Q,
        o_qfin = o_qf + 2 * Q, o_fl = o_qfin + 2 * Q;
   if (tr) {
-    memset(tr, 0, (size_t)P2V_TRACE_WORDS(r, nsteps, Q) * 8);
+    memset(tr, 0, (size_t)P2V_TRACE_WORDS(r, nsteps, Q, C->nluts) * 8);
     for (int i = 0; i < 4; i++) trace_put(tr, o_pi + i, ch.pi_hash[i]);
     for (int i = 0; i < r; i++) { trace_put(tr, o_b + i, ch.betas[i]); trace_put(tr, o_g + i, ch.gammas[i]); trace_put(tr, o_a + i, ch.alphas[i]); }
     for (int i = 0; i < ch.ndeltas && i < r; i++) { trace_put(tr, o_d + 4 * i, ch.deltas[i].A); trace_put(tr, o_d + 4 * i + 1, ch.deltas[i].B); trace_put(tr, o_d + 4 * i + 2, ch.deltas[i].alpha); trace_put(tr, o_d + 4 * i + 3, ch.deltas[i].delta); }
@@ -1111,7 +1112,10 @@ __attribute__((noinline)) static int verify_body(const circuit_t* C, const proof
   }
   /* eqs_ok: checkCombinedPlonkEquations', Plonk/Verifier.hs:35-51 */
   clist cons = {0}; cons.m = m_;
+  if (tr && C->nluts > 0) cons.lutre = (F*)aalloc(m_, (size_t)r * C->nluts * sizeof(F));
+  if (cons.lutre) memset(cons.lutre, 0, (size_t)r * C->nluts * sizeof(F));
   eval_all_constraints(m_, C, P, &ch, &cons);
+  if (cons.lutre) for (int i = 0; i < r * C->nluts; i++) trace_put(tr, o_fl + 1 + i, cons.lutre[i]);
   long nn = 1L << C->degree_bits;
   E zeta_n = Epow(ch.zeta, nn);
   int nqchunks = C->qdf > 0 ? (P->n_quot + C->qdf - 1) / C->qdf : 0;
@@ -1189,7 +1193,7 @@ or_proof* or_proof_load(const char* proof, size_t plen) {
 }
 void or_proof_free(or_proof* p) { if (p) { afree(&p->p.mem); free(p); } }
 
-/* status of verifyProof; trace (optional) gets P2V_TRACE_WORDS(r,S,Q) words.
+/* status of verifyProof; trace (optional) gets P2V_TRACE_WORDS(r,S,Q,L) words.
  * full_trace != 0 computes every trace value even past a deciding failure. */
 int or_verify(const or_circuit* c, const or_proof* p, uint64_t* trace, int full_trace) {
   int s = verify_impl(&c->c, &p->p, trace, full_trace);
@@ -1202,7 +1206,7 @@ int or_trace_words(const or_circuit* c) {
   if (setjmp(jb)) { g_jb = saved; return -1; }
   int ar[64]; int S = expand_strategy(&c->c, ar);
   g_jb = saved;
-  return P2V_TRACE_WORDS(c->c.r, S, c->c.nqueries);
+  return P2V_TRACE_WORDS(c->c.r, S, c->c.nqueries, c->c.nluts);
 }
 
 /* helpers exposed for unit tests */

@@ -18,6 +18,7 @@ extern "C" __global__ void k_phase1(DevCircuit, int, int);
 extern "C" __global__ void k_merkle(DevCircuit);
 extern "C" __global__ void k_fri(DevCircuit);
 extern "C" __global__ void k_vanish(DevCircuit);
+extern "C" __global__ void k_lut(DevCircuit);
 extern "C" __global__ void k_vanish_final(DevCircuit);
 extern "C" __global__ void k_status(DevCircuit, int8_t*, uint64_t*, int64_t);
 
@@ -28,8 +29,8 @@ thread_local std::string g_err;
 int fail(int code, const std::string& msg) { g_err = msg; return code; }
 
 // per-kernel timing slots; k_fri and k_vanish run on the side stream concurrently with k_merkle
-const char* kKernelNames = "k_transpose,k_phase1,k_merkle,k_fri,k_vanish,k_status,k_vanish_final";
-constexpr int kNumKernels = 7;
+const char* kKernelNames = "k_transpose,k_phase1,k_merkle,k_fri,k_vanish,k_status,k_vanish_final,k_lut";
+constexpr int kNumKernels = 8;
 
 struct DevBuf {
   void* p = nullptr;
@@ -59,8 +60,8 @@ struct p2v_verifier {
   size_t max_batch = 0, Bmax = 0;
   DevCircuit dc{};
   std::vector<DevBuf> bufs;
-  DevBuf in, soa, chal, leafdig, mk, fbits, qvals, van, vparts, res, trace;
-  DevBuf t_cs, t_kis, t_gkind, t_gpar, t_ggrp, t_gwoff, t_w, t_gs, t_ge, t_lin, t_lout, t_loff, t_llen, t_tw, t_ops, t_vit;
+  DevBuf in, soa, chal, leafdig, mk, fbits, qvals, van, vparts, lutre, lutpart, res, trace;
+  DevBuf t_cs, t_kis, t_gkind, t_gpar, t_ggrp, t_gwoff, t_w, t_gs, t_ge, t_lin, t_lout, t_loff, t_llen, t_tw, t_ops, t_vit, t_rin, t_rout, t_roff, t_rch, t_pbase;
   hipEvent_t ev[2 * kNumKernels];   // start/end per kernel
   hipEvent_t dep_p1 = nullptr, dep_side = nullptr;
   hipStream_t side = nullptr;
@@ -175,8 +176,8 @@ int p2v_device_count(void) {
 void p2v_verifier_free(p2v_verifier* v) {
   if (!v) return;
   (void)hipSetDevice(v->device);
-  for (DevBuf* b : {&v->in, &v->soa, &v->chal, &v->leafdig, &v->mk, &v->fbits, &v->qvals, &v->van, &v->vparts, &v->res, &v->trace, &v->t_cs, &v->t_kis,
-                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit})
+  for (DevBuf* b : {&v->in, &v->soa, &v->chal, &v->leafdig, &v->mk, &v->fbits, &v->qvals, &v->van, &v->vparts, &v->lutre, &v->res, &v->trace, &v->t_cs, &v->t_kis,
+                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit, &v->t_rin, &v->t_rout, &v->t_roff, &v->t_rch, &v->t_pbase, &v->lutpart})
     b->free_();
   if (v->timed) for (auto& e : v->ev) (void)hipEventDestroy(e);
   if (v->dep_p1) (void)hipEventDestroy(v->dep_p1);
@@ -233,6 +234,29 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   gwoff.push_back((int32_t)wts.size());
   std::vector<uint64_t> lin, lout; std::vector<int64_t> loff, llen;
   for (size_t t = 0; t < C.lut_in.size(); t++) { loff.push_back((int64_t)lin.size()); llen.push_back((int64_t)C.lut_in[t].size()); lin.insert(lin.end(), C.lut_in[t].begin(), C.lut_in[t].end()); lout.insert(lout.end(), C.lut_out[t].begin(), C.lut_out[t].end()); }
+  // evalFinalRE (Lookups.hs:103-109): cur = sum_i delta^(N-1-i) (inp_i + B out_i) over the table
+  // padded to N = ceil(len / slots) * slots entries with its FIRST entry.  Stored reversed
+  // (index t = N-1-i is the power of delta) and zero-filled to a multiple of P2V_LUT_CHUNK, so
+  // the device evaluates it as sum_c delta^(16c) sum_j delta^j e'_(16c+j) (baby/giant steps).
+  std::vector<uint32_t> rin, rout; std::vector<int64_t> roff; std::vector<int32_t> rch, pbase{0};
+  {
+    const int64_t slots = C.num_routed / 3;
+    for (size_t t = 0; t < C.lut_in.size(); t++) {
+      const auto& li = C.lut_in[t]; const auto& lo = C.lut_out[t];
+      const int64_t len = (int64_t)li.size();
+      const int64_t N = slots > 0 ? (len + slots - 1) / slots * slots : 0;
+      bool small = len > 0;
+      for (int64_t i = 0; i < len && small; i++) small = li[i] < (1u << 24) && lo[i] < (1u << 24);
+      const int64_t nch = small ? (N + P2V_LUT_CHUNK - 1) / P2V_LUT_CHUNK : 0;
+      roff.push_back((int64_t)rin.size()); rch.push_back((int32_t)nch);
+      pbase.push_back(pbase.back() + (int32_t)((nch + P2V_LUT_PIECE - 1) / P2V_LUT_PIECE));
+      for (int64_t k = 0; k < nch * P2V_LUT_CHUNK; k++) {
+        const int64_t i = N - 1 - k, ii = i < len ? i : 0;
+        rin.push_back(k < N ? (uint32_t)li[ii] : 0u);
+        rout.push_back(k < N ? (uint32_t)lo[ii] : 0u);
+      }
+    }
+  }
   std::vector<uint64_t> tw(256 * (size_t)(d.S ? d.S : 1), 0);
   for (int s = 0; s < d.S; s++) {
     int ab = C.arities[s];
@@ -283,6 +307,8 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
 #define UP(buf, vec) if (e == hipSuccess) e = upload(buf, vec)
   UP(v->t_cs, C.cs_cap); UP(v->t_kis, C.k_is); UP(v->t_gkind, gkind); UP(v->t_gpar, gpar); UP(v->t_ggrp, ggrp); UP(v->t_gwoff, gwoff);
   UP(v->t_w, wts); UP(v->t_gs, gs); UP(v->t_ge, ge); UP(v->t_lin, lin); UP(v->t_lout, lout); UP(v->t_loff, loff); UP(v->t_llen, llen); UP(v->t_tw, tw); UP(v->t_ops, ops); UP(v->t_vit, vit);
+  UP(v->t_rin, rin); UP(v->t_rout, rout); UP(v->t_roff, roff); UP(v->t_rch, rch); UP(v->t_pbase, pbase);
+  d.n_lut_pieces = pbase.back();
 #undef UP
   const size_t B = v->Bmax;
   const size_t chw = (size_t)(4 + 7 * d.r + 4 + 2 * d.S + 1 + d.Q + 4);
@@ -295,6 +321,8 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (e == hipSuccess) e = v->qvals.alloc((size_t)d.Q * 6 * B * 8);
   if (e == hipSuccess) e = v->van.alloc((size_t)(1 + 4 * d.r) * B * 8);
   if (e == hipSuccess) e = v->vparts.alloc((size_t)d.n_vitems * 2 * d.r * B * 8);
+  if (e == hipSuccess) e = v->lutre.alloc((size_t)d.r * (d.nluts ? d.nluts : 1) * B * 8);
+  if (e == hipSuccess) e = v->lutpart.alloc((size_t)d.r * (d.n_lut_pieces ? d.n_lut_pieces : 1) * B * 8);
   if (e == hipSuccess) e = v->res.alloc(B);
   if (e == hipSuccess) e = v->trace.alloc((size_t)C.trace_words * B * 8);
   if (e == hipSuccess) { for (auto& x : v->ev) { e = hipEventCreate(&x); if (e != hipSuccess) break; } v->timed = e == hipSuccess; }
@@ -306,9 +334,10 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   d.gate_par = (const int64_t*)v->t_gpar.p; d.gate_grp = (const int32_t*)v->t_ggrp.p; d.gate_woff = (const int32_t*)v->t_gwoff.p;
   d.weights = (const uint64_t*)v->t_w.p; d.grp_start = (const int32_t*)v->t_gs.p; d.grp_end = (const int32_t*)v->t_ge.p;
   d.lut_in = (const uint64_t*)v->t_lin.p; d.lut_out = (const uint64_t*)v->t_lout.p; d.lut_off = (const int64_t*)v->t_loff.p; d.lut_len = (const int64_t*)v->t_llen.p;
+  d.lut_rin = (const uint32_t*)v->t_rin.p; d.lut_rout = (const uint32_t*)v->t_rout.p; d.lut_roff = (const int64_t*)v->t_roff.p; d.lut_rchunks = (const int32_t*)v->t_rch.p; d.lut_pbase = (const int32_t*)v->t_pbase.p;
   d.twiddles = (const uint64_t*)v->t_tw.p; d.tops = (const int32_t*)v->t_ops.p; d.vitems = (const int32_t*)v->t_vit.p;
   d.soa = (const uint64_t*)v->soa.p; d.chal = (uint64_t*)v->chal.p; d.leafdig = (uint64_t*)v->leafdig.p; d.mk_ok = (uint8_t*)v->mk.p;
-  d.fri_bits = (uint32_t*)v->fbits.p; d.qvals = (uint64_t*)v->qvals.p; d.van = (uint64_t*)v->van.p; d.vparts = (uint64_t*)v->vparts.p;
+  d.fri_bits = (uint32_t*)v->fbits.p; d.qvals = (uint64_t*)v->qvals.p; d.van = (uint64_t*)v->van.p; d.vparts = (uint64_t*)v->vparts.p; d.lutre = (uint64_t*)v->lutre.p; d.lutpart = (uint64_t*)v->lutpart.p;
   *out = v;
   return P2V_OK;
 }
@@ -357,6 +386,9 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   // long-latency waves) on the side stream, concurrently
   HCK(hipEventRecord(v->dep_p1, st));
   HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));
+  T0(7, sd);
+  if (d.n_lut_pieces > 0) k_lut<<<(d.r * d.n_lut_pieces * NPB + 3) / 4, 256, 0, sd>>>(d);
+  T1(7, sd);
   T0(4, sd);
   k_vanish<<<(d.n_vitems * NPB + 3) / 4, 256, 0, sd>>>(d);
   T1(4, sd);

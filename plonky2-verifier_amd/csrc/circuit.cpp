@@ -284,7 +284,7 @@ Circuit parse_circuit(const JVal& common, const JVal& vkey) {
   w += q * C.num_queries;
   L.words = w;
   const int S = (int)C.arities.size(), Q = C.num_queries, r = C.r;
-  C.trace_words = 4 + 3 * r + 4 * r + 4 + 2 * S + 1 + Q + 4 * r + 6 * Q + 1;
+  C.trace_words = 4 + 3 * r + 4 * r + 4 + 2 * S + 1 + Q + 4 * r + 6 * Q + 1 + r * (int64_t)C.lut_in.size();
   return C;
 }
 

@@ -6,6 +6,8 @@
 
 #define P2V_MAX_STEPS 8
 #define P2V_MAX_R 4
+#define P2V_LUT_CHUNK 16   // baby steps of the LUT evaluation
+#define P2V_LUT_PIECE 256  // chunks per k_lut work unit (4096 table entries)
 
 struct DevCircuit {
   int32_t B;            // lane stride (batch padded to a multiple of 64)
@@ -44,6 +46,15 @@ struct DevCircuit {
   const uint64_t* lut_out;
   const int64_t* lut_off;          // [nluts]
   const int64_t* lut_len;
+  // evalFinalRE fast path (Lookups.hs:103-109): per LUT the padded entry sequence reversed
+  // (coefficient of delta^t) and zero-filled to P2V_LUT_CHUNK, as u32; lut_rchunks[k] = 0 when
+  // an entry is >= 2^24 (then the per-entry Horner over lut_in/lut_out is used)
+  const uint32_t* lut_rin;
+  const uint32_t* lut_rout;
+  const int64_t* lut_roff;         // [nluts]
+  const int32_t* lut_rchunks;      // [nluts]
+  const int32_t* lut_pbase;        // [nluts + 1] first k_lut piece of each table
+  int32_t n_lut_pieces;
   const uint64_t* twiddles;        // per step: omega_{a}^{-j}, j < 2^a  (offset 256*s)
   const int32_t* tops;             // transcript op program [ntops][3] (see TOP_*)
   int32_t ntops;
@@ -58,6 +69,8 @@ struct DevCircuit {
   uint64_t* qvals;                 // [Q][6][B]: initial, folded, final (F^2 each)
   uint64_t* van;                   // [1 + 4r][B]: eqs_ok, C_i, quotient_i
   uint64_t* vparts;                // [n_vitems][2r][B]: per-item partial alpha-sums
+  uint64_t* lutre;                 // [r][nluts][B]: evalFinalRE values (debug trace)
+  uint64_t* lutpart;               // [r][n_lut_pieces][B]: k_lut partial sums
 };
 
 // transcript op program (built on the host from the circuit; uniform across the batch)

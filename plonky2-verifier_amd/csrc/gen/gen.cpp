@@ -600,7 +600,7 @@ char* dupstr(const std::string& s) { char* p = (char*)malloc(s.size() + 1); memc
 
 extern "C" {
 
-// spec: degree_bits, num_public_inputs, lookups (0/1), circuit_seed
+// spec: degree_bits, num_public_inputs, lookups (0 none, 1/2/3 table sets, see below), circuit_seed
 void* p2v_gen_circuit_new(int degree_bits, int num_pis, int lookups, uint64_t circuit_seed, int num_queries, int pow_bits) {
   try {
     auto* C = new Circuit();
@@ -611,8 +611,10 @@ void* p2v_gen_circuit_new(int degree_bits, int num_pis, int lookups, uint64_t ci
       C->nlp = 7;
       std::vector<std::pair<u64, u64>> t8, t16;
       for (u64 i = 0; i < 256; i++) t8.push_back({i, (i * i + 7) & 255});
-      int big = lookups > 1 ? 65536 : 1000;
-      for (u64 i = 0; i < (u64)big; i++) t16.push_back({i, 0});
+      // 1: 1000-entry table; 2: 2^16-entry range table (BASELINE C3); 3: 300 entries with
+      // field-sized outputs (exercises the verifier's generic evalFinalRE path)
+      int big = lookups == 2 ? 65536 : lookups == 3 ? 300 : 1000;
+      for (u64 i = 0; i < (u64)big; i++) t16.push_back({i, lookups == 3 ? (i * 0x9E3779B97F4A7C15ULL) % 0xFFFFFFFF00000001ULL : 0});
       C->luts.push_back(t8); C->luts.push_back(t16);
     }
     build_circuit(*C);

@@ -489,6 +489,7 @@ extern "C" __global__ void __launch_bounds__(256) k_status(DevCircuit c, int8_t*
         tr[k++] = qv[(int64_t)(2 * j + 1) * c.B];
       }
     tr[k++] = (uint64_t)(eqs_ok ? 1 : 0) | ((uint64_t)(pow_ok ? 1 : 0) << 1);
+    for (int i = 0; i < r * c.nluts; i++) tr[k++] = c.lutre[(int64_t)i * c.B + p];
     (void)S;
   }
 }

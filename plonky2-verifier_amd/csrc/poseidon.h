@@ -9,6 +9,10 @@
 #pragma once
 #include "gl.h"
 #include "poseidon_constants.h"
+#include "pasm.h"
+#ifndef P2V_POSEIDON_ASMBLK
+#define P2V_POSEIDON_ASMBLK 0   // measured: no faster in the verifier kernels (VGPR pressure), see DESIGN.md §5.1
+#endif
 
 namespace p2 {
 
@@ -60,9 +64,10 @@ __host__ __device__ __forceinline__ uint64_t sbox(uint64_t x) {
 #define P2_UNROLL _Pragma("GCC unroll 12")
 #endif
 
-// ah * 2^32 + al (al, ah < 2^43) -> [0, 2^64): with ah = ah_hi 2^32 + ah_lo the value is
+// ah * 2^32 + al (al, ah < 2^63) -> [0, 2^64): with ah = ah_hi 2^32 + ah_lo the value is
 // ah_hi 2^64 + ah_lo 2^32 + al == ah_hi (2^32 - 1) + al + ah_lo 2^32 (mod p); the first two
-// terms stay below 2^44, so one wrap fix-up suffices (v_mad_u64_u32 + 3 VALU).
+// terms stay below 2^64 and adding ah_lo 2^32 wraps at most once, after which the sum is
+// below 2^63, so one wrap fix-up suffices (v_mad_u64_u32 + 3 VALU).
 __host__ __device__ __forceinline__ uint64_t mds_reduce(uint64_t al, uint64_t ah) {
   const uint64_t t = (ah >> 32) * 0xFFFFFFFFULL + al;
   const uint64_t r = t + (ah << 32);
@@ -183,6 +188,12 @@ __device__ __forceinline__ void mds_acc(const uint64_t* s, uint64_t& al, uint64_
 // t[I..E) = (M s)[I..E) + k (k = the next round's constants, split into halves)
 template <int I, int E>
 __device__ __forceinline__ void mds_rows(const uint64_t* s, uint64_t* t, const uint64_t* kl, const uint64_t* kh) {
+#if P2V_POSEIDON_ASMBLK
+  if constexpr (I < E) {
+    t[I] = p2asm::mds_row<I>(s, kl[I], kh[I]);
+    mds_rows<I + 1, E>(s, t, kl, kh);
+  }
+#else
   if constexpr (I < E) {
     constexpr uint32_t C = mds_coeff(I, 0);
     uint64_t al = madk_s<C>((uint32_t)s[0], kl[I]);
@@ -191,6 +202,15 @@ __device__ __forceinline__ void mds_rows(const uint64_t* s, uint64_t* t, const u
     t[I] = reduce_rows(al, ah);
     mds_rows<I + 1, E>(s, t, kl, kh);
   }
+#endif
+}
+__device__ __forceinline__ uint64_t sbox_dev(uint64_t x) {
+#if P2V_POSEIDON_ASMBLK
+  const uint64_t x2 = p2asm::mul_blk(x, x), x3 = p2asm::mul_blk(x, x2), x4 = p2asm::mul_blk(x2, x2);
+  return p2asm::mul_blk(x3, x4);
+#else
+  return sbox(x);
+#endif
 }
 // round r: s -> t (s is clobbered by the S-boxes); t = M sbox(s) + rc[r + 1].
 // zh0: round 0 with state words 8..11 entering as 0 (their S-box outputs are constants).
@@ -199,16 +219,16 @@ template <bool FULL>
 __device__ __forceinline__ void round_pp(uint64_t* s, uint64_t* t, int r, bool zh0, int g) {
   if (FULL) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) s[i] = sbox(s[i]);
+    for (int i = 0; i < 8; i++) s[i] = sbox_dev(s[i]);
     if (zh0) {
 #pragma unroll
       for (int i = 8; i < 12; i++) s[i] = c_zh.z[i - 8];
     } else {
 #pragma unroll
-      for (int i = 8; i < 12; i++) s[i] = sbox(s[i]);
+      for (int i = 8; i < 12; i++) s[i] = sbox_dev(s[i]);
     }
   } else {
-    s[0] = sbox(s[0]);
+    s[0] = sbox_dev(s[0]);
   }
   const uint64_t* kl = c_rc_split.lo + 12 * (r + 1);
   const uint64_t* kh = c_rc_split.hi + 12 * (r + 1);

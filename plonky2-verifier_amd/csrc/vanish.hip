@@ -372,6 +372,38 @@ __device__ void item_pp(const DevCircuit& c, Acc& T, int j, int p) {
 }
 
 // lookup terms of challenge round j, Plonk/Lookups.hs:45-132
+// evalFinalRE (Lookups.hs:103-109) as Ain(delta) + B Aout(delta), where Ain / Aout have the
+// table's (padded, reversed) inputs / outputs as coefficients (exactly the reference's Horner
+// sum, reassociated).  Baby steps: delta^0..15 per lane; each 16-entry chunk is a dot product
+// of u24 wave-uniform coefficients (scalar loads) with the powers' 32-bit halves, accumulated
+// exactly in 64 bits (< 16 2^24 2^32 = 2^60) and reduced once; giant steps: Horner in
+// delta^16 over the chunks.  ~8 VALU per table entry instead of ~50.  k_lut evaluates pieces
+// of P2V_LUT_PIECE chunks, P_s = sum_{c in piece s} delta^(16 (c - c0_s)) (Cin_c + B Cout_c),
+// on many waves; item_lookup combines them by Horner in delta^(16 P2V_LUT_PIECE).
+__device__ __noinline__ uint64_t lut_piece(const DevCircuit& c, int k, int c0, int c1, uint64_t dde, uint64_t dB) {
+  constexpr int M = P2V_LUT_CHUNK;
+  uint64_t pw[M];
+  pw[0] = 1;
+#pragma unroll
+  for (int j = 1; j < M; j++) pw[j] = gl::mul(pw[j - 1], dde);
+  const uint64_t dM = gl::mul(pw[M - 1], dde);
+  const uint32_t* ri = c.lut_rin + c.lut_roff[k];
+  const uint32_t* ro = c.lut_rout + c.lut_roff[k];
+  uint64_t ai = 0, ao = 0;
+  for (int ch = c1 - 1; ch >= c0; ch--) {
+    uint64_t il = 0, ih = 0, ol = 0, oh = 0;
+#pragma unroll
+    for (int j = 0; j < M; j++) {
+      const uint64_t ci = ri[M * ch + j], co = ro[M * ch + j];
+      il += ci * (uint32_t)pw[j]; ih += ci * (uint32_t)(pw[j] >> 32);
+      ol += co * (uint32_t)pw[j]; oh += co * (uint32_t)(pw[j] >> 32);
+    }
+    ai = gl::add(gl::mul(ai, dM), gl::canon(p2::mds_reduce(il, ih)));
+    ao = gl::add(gl::mul(ao, dM), gl::canon(p2::mds_reduce(ol, oh)));
+  }
+  return gl::add(ai, gl::mul(dB, ao));
+}
+
 __device__ void item_lookup(const DevCircuit& c, Acc& T, int j, int p) {
   const E one = gl::eb(1);
   const int nlp = c.nlp, nsldc = nlp - 1;
@@ -394,13 +426,24 @@ __device__ void item_lookup(const DevCircuit& c, Acc& T, int j, int p) {
   T.push(gl::emul(sel(2), sldc(0)));
   T.push(gl::emul(sel(2), re));
   for (int k = 0; k < c.nluts; k++) {   // evalFinalRE, :103-109
-    const int64_t len = c.lut_len[k], off = c.lut_off[k];
-    const int64_t padded = ((len + slots3 - 1) / slots3) * slots3;
-    uint64_t cur = 0;
-    for (int64_t i = 0; i < padded; i++) {
-      const int64_t jj = i < len ? i : 0;
-      cur = gl::add(gl::mul(dde, cur), gl::add(c.lut_in[off + jj], gl::mul(dB, c.lut_out[off + jj])));
+    uint64_t cur;
+    if (c.lut_rchunks[k] > 0) {   // combine the k_lut pieces
+      const int pb = c.lut_pbase[k], np = c.lut_pbase[k + 1] - pb;
+      uint64_t dL = dde;
+      for (int e = 1; e < P2V_LUT_CHUNK * P2V_LUT_PIECE; e <<= 1) dL = gl::mul(dL, dL);   // delta^(16 * 256)
+      const uint64_t* part = c.lutpart + ((int64_t)j * c.n_lut_pieces + pb) * c.B + p;
+      cur = part[(int64_t)(np - 1) * c.B];
+      for (int s2 = np - 2; s2 >= 0; s2--) cur = gl::add(gl::mul(cur, dL), part[(int64_t)s2 * c.B]);
+    } else {
+      const int64_t len = c.lut_len[k], off = c.lut_off[k];
+      const int64_t padded = ((len + slots3 - 1) / slots3) * slots3;
+      cur = 0;
+      for (int64_t i = 0; i < padded; i++) {
+        const int64_t jj = i < len ? i : 0;
+        cur = gl::add(gl::mul(dde, cur), gl::add(c.lut_in[off + jj], gl::mul(dB, c.lut_out[off + jj])));
+      }
     }
+    c.lutre[((int64_t)j * c.nluts + k) * c.B + p] = cur;
     T.push(gl::emul(sel(4 + k), gl::esub(re, gl::eb(cur))));
   }
   {
@@ -470,6 +513,23 @@ __device__ void vanish_item(const DevCircuit& c, int it, int p) {
 }
 
 }  // namespace
+
+// evalFinalRE pieces: one wave = (challenge round j, piece, 64 proofs)
+extern "C" __global__ void __launch_bounds__(256) k_lut(DevCircuit c) {
+  const int lane = threadIdx.x & 63;
+  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int NPB = c.B >> 6;
+  if (unit >= c.r * c.n_lut_pieces * NPB) return;
+  __builtin_amdgcn_s_setprio(2);   // side stream, concurrent with k_merkle (see k_vanish)
+  const int jp = unit / NPB, p = (unit % NPB) * 64 + lane;
+  const int j = jp / c.n_lut_pieces, pi = jp % c.n_lut_pieces;
+  int k = 0;
+  while (c.lut_pbase[k + 1] <= pi) k++;
+  const int s2 = pi - c.lut_pbase[k];
+  const int c0 = s2 * P2V_LUT_PIECE, c1 = min(c0 + P2V_LUT_PIECE, (int)c.lut_rchunks[k]);
+  const uint64_t dB = chal(c, CH_DELTA(c) + 4 * j + 1, p), dde = chal(c, CH_DELTA(c) + 4 * j + 3, p);
+  c.lutpart[(int64_t)jp * c.B + p] = lut_piece(c, k, c0, c1, dde, dB);
+}
 
 // one wave = (item, 64 proofs); items are wave-uniform, heaviest first (host order)
 extern "C" __global__ void __launch_bounds__(256) k_vanish(DevCircuit c) {

@@ -29,7 +29,7 @@ from typing import Iterable, List, Optional, Sequence, Union
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libp2v.so")
+LIB_PATH = os.environ.get("P2V_LIB") or os.path.join(_HERE, "libp2v.so")   # P2V_LIB: A/B measurement builds
 
 # per-proof status codes (include/p2v.h)
 ACCEPT = 1

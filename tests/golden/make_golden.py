@@ -58,14 +58,14 @@ def main():
         if key not in circuits:
             cname = f"circuit_n{nb}_lk{lk}_pow{pb}"
             circuits[key] = cname
-            with gzip.open(os.path.join(HERE, cname + "_common.json.gz"), "wb") as f:
+            with gzip.GzipFile(os.path.join(HERE, cname + "_common.json.gz"), "wb", mtime=0) as f:
                 f.write(gc.common)
-            with gzip.open(os.path.join(HERE, cname + "_vkey.json.gz"), "wb") as f:
+            with gzip.GzipFile(os.path.join(HERE, cname + "_vkey.json.gz"), "wb", mtime=0) as f:
                 f.write(gc.vkey)
         proof = gc.proof(ws, ps, flags)
         if mut:
             proof = mutate(proof, lambda d: apply(mut, d))
-        with gzip.open(os.path.join(HERE, name + "_proof.json.gz"), "wb") as f:
+        with gzip.GzipFile(os.path.join(HERE, name + "_proof.json.gz"), "wb", mtime=0) as f:
             f.write(proof)
         st, tr = O.verify_json(gc.common, gc.vkey, proof, trace=True)
         index.append({"name": name, "circuit": circuits[key], "status": int(st), "trace": [str(int(x)) for x in tr]})

@@ -30,7 +30,9 @@ def _cases(gc):
     return out + _reject_cases(gc)
 
 
-@pytest.mark.parametrize("nb,lk", [(6, 0), (6, 1), (8, 0)])
+# lk: 0 none; 1 a 256- and a 1000-entry table; 2 a 256- and a 2^16-entry table (BASELINE C3's
+# tables: the baby/giant-step evalFinalRE); 3 field-sized table outputs (the generic path)
+@pytest.mark.parametrize("nb,lk", [(6, 0), (6, 1), (6, 2), (6, 3), (8, 0)])
 def test_gpu_matches_oracle_status_and_trace(p2v, nb, lk):
     O = oracle()
     gc = gen_circuit(nb, 4, lk)
@@ -131,3 +133,29 @@ def test_verify_proof_api(p2v):
     assert e.value.status == -3
     out = p2v.verify_proof_batch(vk, [gc.proof(1, 1), gc.proof(1, 6, flags=4)])
     assert out == [True, False]
+
+
+def test_gpu_c3_lookup_batch_full_size(p2v):
+    """BASELINE configs[2] shape: 65 536 proofs of the lookup circuit (LookupGate +
+    LookupTableGate, a 256-entry and a 2^16-entry table) at degree_bits 12 in one batch.
+    Every valid proof accepts, corrupted lanes reject with the oracle's status, and the
+    full trace of sampled lanes (incl. every evalFinalRE value) equals the oracle's."""
+    O = oracle()
+    gc = gen_circuit(12, 4, 2)
+    pool = [gc.proof(1, 1), gc.proof(2, 2), gc.proof(1, 5, flags=2)]
+    expect = [O.verify_json(gc.common, gc.vkey, p) for p in pool]
+    assert expect == [1, 1, 0]
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    packed = vk.pack_many(pool)
+    B = 65536
+    idx = np.zeros(B, dtype=np.int64)
+    idx[1::2] = 1
+    idx[[77, 40000, 65535]] = 2
+    bv = p2v.BatchVerifier(vk, 0, B)
+    res, tr = bv.run(np.ascontiguousarray(packed[idx]), trace=True)
+    assert np.array_equal(res, np.array(expect, dtype=np.int8)[idx])
+    for k in range(len(pool)):
+        st, otr = O.verify_json(gc.common, gc.vkey, pool[k], trace=True)
+        lanes = np.nonzero(idx == k)[0]
+        for lane in (lanes[0], lanes[-1]):
+            assert np.array_equal(tr[lane], otr), (k, lane)
