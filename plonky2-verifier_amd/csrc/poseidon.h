@@ -281,6 +281,7 @@ __device__ __forceinline__ void permute_dev(uint64_t s[12], bool zh = false, int
 }
 #elif defined(__HIPCC__)
 __device__ void permute_dev(uint64_t s[12], bool zh = false, int gm = 7);   // device-only
+namespace dv { template <uint32_t C> __device__ uint64_t madk(uint32_t a, uint64_t acc); }
 #endif
 
 // Hash/Poseidon.hs:42-46.  Inputs may be any value < 2^64; outputs are canonical.

@@ -37,61 +37,72 @@ __device__ __forceinline__ uint64_t bcast64(uint64_t v, int src) {
   return ((uint64_t)bcast32((uint32_t)(v >> 32), src) << 32) | bcast32((uint32_t)v, src);
 }
 
-// this lane's round constants (words 3t..3t+2 of round r): in the natural table layout
-// (Hash/Constants.hs) they are contiguous, so each lane does a plain vector load.  The caller
-// prefetches one round ahead so the load latency hides behind the current round.
-__device__ __forceinline__ void lane_rc(int r, int t, uint64_t rc[3]) {
-  const uint64_t* R = p2::c_round_constants + 12 * r + 3 * t;
+// this lane's round constants (words 3t..3t+2 of round r) as 32-bit halves: they start the
+// MDS row accumulators of round r-1 (the constant addition folded into the previous MDS, as
+// in p2::permute_dev).  In the natural table layout they are contiguous, so each lane does a
+// plain vector load; the caller prefetches one round ahead.
+__device__ __forceinline__ void lane_rc(int r, int t, uint64_t kl[3], uint64_t kh[3]) {
+  const uint64_t* L = p2::c_rc_split.lo + 12 * r + 3 * t;
+  const uint64_t* H = p2::c_rc_split.hi + 12 * r + 3 * t;
 #pragma unroll
-  for (int k = 0; k < 3; k++) rc[k] = R[k];
+  for (int k = 0; k < 3; k++) { kl[k] = L[k]; kh[k] = H[k]; }
 }
 
-__device__ __forceinline__ void mds(uint64_t x[3], int t) {
+// one MDS row M of this lane (global row 3t + M): the 12 terms in (rotation d, word k) order
+template <int M, int Q>
+__device__ __forceinline__ void qrow(const uint64_t (&X)[4][3], uint64_t& al, uint64_t& ah, uint64_t c00) {
+  if constexpr (Q < 12) {
+    constexpr int d = Q / 3, k = Q % 3;
+    constexpr int idx = ((3 * d + k - M) % 12 + 12) % 12;
+    if constexpr (M == 0 && Q == 0) {   // the diagonal entry: 25 on global row 0, else 17
+      al += (uint64_t)(uint32_t)X[d][k] * c00;
+      ah += (X[d][k] >> 32) * c00;
+    } else {
+      al = p2::dv::madk<p2::MDS_CIRC[idx]>((uint32_t)X[d][k], al);
+      ah = p2::dv::madk<p2::MDS_CIRC[idx]>((uint32_t)(X[d][k] >> 32), ah);
+    }
+    qrow<M, Q + 1>(X, al, ah, c00);
+  }
+}
+
+// x <- M x + k (k = the next round's constants of this lane's rows, split into halves)
+__device__ __forceinline__ void mds(uint64_t x[3], int t, const uint64_t kl[3], const uint64_t kh[3]) {
   uint64_t X[4][3];
 #pragma unroll
   for (int k = 0; k < 3; k++) { X[0][k] = x[k]; X[1][k] = rot64<1>(x[k]); X[2][k] = rot64<2>(x[k]); X[3][k] = rot64<3>(x[k]); }
   const uint64_t c00 = t == 0 ? 25 : 17;   // circ[0] (+ diag[0] on row 0)
-  uint64_t out[3];
-#pragma unroll
-  for (int m = 0; m < 3; m++) {
-    uint64_t al = 0, ah = 0;
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        const int idx = ((3 * d + k - m) % 12 + 12) % 12;
-        const uint64_t c = (m == 0 && d == 0 && k == 0) ? c00 : (uint64_t)p2::MDS_CIRC[idx];
-        al += (uint64_t)(uint32_t)X[d][k] * c;
-        ah += (X[d][k] >> 32) * c;
-      }
-    }
-    out[m] = p2::mds_reduce(al, ah);
-  }
-#pragma unroll
-  for (int k = 0; k < 3; k++) x[k] = out[k];
+  uint64_t al0 = kl[0], ah0 = kh[0], al1 = kl[1], ah1 = kh[1], al2 = kl[2], ah2 = kh[2];
+  qrow<0, 0>(X, al0, ah0, c00);
+  qrow<1, 0>(X, al1, ah1, c00);
+  qrow<2, 0>(X, al2, ah2, c00);
+  x[0] = p2::mds_reduce(al0, ah0);
+  x[1] = p2::mds_reduce(al1, ah1);
+  x[2] = p2::mds_reduce(al2, ah2);
 }
 
 // the quad's permutation; x = this lane's three words (inputs < 2^64, outputs canonical)
 __device__ __forceinline__ void permute(uint64_t x[3], int t) {
-  uint64_t rc[3], nrc[3];
-  lane_rc(0, t, nrc);
+  {
+    const uint64_t* R = p2::c_round_constants + 3 * t;
+#pragma unroll
+    for (int k = 0; k < 3; k++) x[k] = p2::add_nc(x[k], R[k]);
+  }
+  uint64_t kl[3], kh[3], nkl[3], nkh[3];
+  lane_rc(1, t, nkl, nkh);
 #pragma unroll 1
   for (int r = 0; r < 30; r++) {
 #pragma unroll
-    for (int k = 0; k < 3; k++) rc[k] = nrc[k];
-    lane_rc(r < 29 ? r + 1 : 29, t, nrc);
+    for (int k = 0; k < 3; k++) { kl[k] = nkl[k]; kh[k] = nkh[k]; }
+    lane_rc(r + 2 <= 30 ? r + 2 : 30, t, nkl, nkh);   // row 30 of the split table is zero
     const bool full = r < 4 || r >= 26;
     if (full) {
 #pragma unroll
-      for (int k = 0; k < 3; k++) x[k] = p2::sbox(p2::add_nc(x[k], rc[k]));
+      for (int k = 0; k < 3; k++) x[k] = p2::sbox(x[k]);
     } else {
-      const uint64_t a = p2::add_nc(x[0], rc[0]);
-      const uint64_t s = p2::sbox(a);   // computed by every lane, kept by lane 0 (word 0)
-      x[0] = t == 0 ? s : a;
-      x[1] = p2::add_nc(x[1], rc[1]);
-      x[2] = p2::add_nc(x[2], rc[2]);
+      const uint64_t s = p2::sbox(x[0]);   // computed by every lane, kept by lane 0 (word 0)
+      x[0] = t == 0 ? s : x[0];
     }
-    mds(x, t);
+    mds(x, t, kl, kh);
   }
 #pragma unroll
   for (int k = 0; k < 3; k++) x[k] = gl::canon(x[k]);

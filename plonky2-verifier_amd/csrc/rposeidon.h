@@ -84,11 +84,12 @@ __device__ __forceinline__ void acc_rot(const Row& R, uint32_t lo, uint32_t hi, 
   al += (uint64_t)ror32<M>(lo) * R.coef[M];
   ah += (uint64_t)ror32<M>(hi) * R.coef[M];
 }
-// sum_m coef[m] ror_m(v), accumulated over the 32-bit halves; even and odd rotations go to
-// separate accumulators (4 independent mad chains) so the scheduler can overlap them
+// (al, ah) += sum_m coef[m] ror_m(v), accumulated over the 32-bit halves; even and odd
+// rotations go to separate accumulators (4 independent mad chains) so the scheduler can
+// overlap them
 __device__ __forceinline__ void conv(const Row& R, uint64_t v, uint64_t& al, uint64_t& ah) {
   const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-  uint64_t al0 = (uint64_t)lo * R.coef[0], ah0 = (uint64_t)hi * R.coef[0];
+  uint64_t al0 = (uint64_t)lo * R.coef[0] + al, ah0 = (uint64_t)hi * R.coef[0] + ah;
   uint64_t al1 = (uint64_t)ror32<1>(lo) * R.coef[1], ah1 = (uint64_t)ror32<1>(hi) * R.coef[1];
   acc_rot<2>(R, lo, hi, al0, ah0); acc_rot<3>(R, lo, hi, al1, ah1);
   acc_rot<4>(R, lo, hi, al0, ah0); acc_rot<5>(R, lo, hi, al1, ah1);
@@ -101,23 +102,29 @@ __device__ __forceinline__ void conv(const Row& R, uint64_t v, uint64_t& al, uin
   ah = ah0 + ah1;
 }
 
-// this lane's round constant (idle lanes read word 11), prefetched one round ahead
-__device__ __forceinline__ uint64_t lane_rc(int r, int L) { return p2::c_round_constants[12 * r + (L < 12 ? L : 11)]; }
+// this lane's round constant (idle lanes read word 11) as 32-bit halves, prefetched one
+// round ahead: it starts the lane's MDS accumulators of the previous round (the constant
+// addition folded into the MDS, as in p2::permute_dev)
+__device__ __forceinline__ void lane_rc(int r, int L, uint64_t& kl, uint64_t& kh) {
+  const int i = 12 * r + (L < 12 ? L : 11);
+  kl = p2::c_rc_split.lo[i];
+  kh = p2::c_rc_split.hi[i];
+}
 
 // the row's permutation; x = this lane's word (inputs < 2^64, outputs canonical)
 __device__ __forceinline__ uint64_t permute(uint64_t x, const Row& R) {
-  uint64_t nrc = lane_rc(0, R.L);
+  x = p2::add_nc(x, p2::c_round_constants[R.L < 12 ? R.L : 11]);
+  uint64_t nkl, nkh;
+  lane_rc(1, R.L, nkl, nkh);
 #pragma unroll 1
   for (int r = 0; r < 30; r++) {
-    const uint64_t rc = nrc;
-    nrc = lane_rc(r < 29 ? r + 1 : 29, R.L);
-    const uint64_t a = p2::add_nc(x, rc);
-    uint64_t al, ah;
+    uint64_t al = nkl, ah = nkh;
+    lane_rc(r + 2 <= 30 ? r + 2 : 30, R.L, nkl, nkh);   // row 30 of the split table is zero
     if (r < 4 || r >= 26) {
-      conv(R, p2::sbox(a), al, ah);
+      conv(R, p2::sbox(x), al, ah);
     } else {
-      conv(R, R.L == 0 ? 0 : a, al, ah);   // words 1..11: independent of the S-box chain
-      const uint64_t s = nbcast64<0>(p2::sbox(a));
+      conv(R, R.L == 0 ? 0 : x, al, ah);   // words 1..11: independent of the S-box chain
+      const uint64_t s = nbcast64<0>(p2::sbox(x));
       al += (uint64_t)(uint32_t)s * R.col0;
       ah += (s >> 32) * R.col0;
     }

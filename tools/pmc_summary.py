@@ -48,6 +48,18 @@ def main():
         out[k] = int(round((2 * f + w) * 1024))
         out[k + "_raw_KiB"] = {"FETCH_SIZE": f, "WRITE_SIZE": w}
     json.dump(out, open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
+    vpath = os.path.join(src, "pmc_valu", "run_counter_collection.csv")
+    if os.path.exists(vpath):
+        valu = {c: per_kernel(vpath, c) for c in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU")}
+        tot = sum(valu["SQ_INSTS_VALU"].values())
+        vout = {"_note": "rocprofv3 PMC SQ counters per launch (median), bench.py --steps 3 --inflight 1, batch = 4096 std "
+                         "proofs; SQ_INSTS_VALU counts wave-level VALU instructions (x4 cycles each at full rate on a "
+                         "SIMD); share = fraction of all VALU instructions of one verification step; round " + tag}
+        for k in sorted(valu["SQ_INSTS_VALU"]):
+            vout[k] = {c: valu[c].get(k) for c in valu}
+            vout[k]["valu_share"] = round(valu["SQ_INSTS_VALU"][k] / tot, 4)
+        json.dump(vout, open(os.path.join(prof, f"{tag}_pmc_valu.json"), "w"), indent=1)
+        print(json.dumps({k: v["valu_share"] for k, v in vout.items() if not k.startswith("_")}, indent=1))
     print(json.dumps({k: v for k, v in out.items() if not k.endswith("_KiB")}, indent=1))
 
 
