@@ -34,6 +34,32 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 METRIC = "Plonky2 proofs verified/sec (std config, 28 FRI queries) at 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# integer VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD per 4 cycles
+# at 2.4 GHz (full-rate ops: v_mad_u64_u32, v_add/sub/cndmask; measured, tools/microbench/rates.hip)
+VALU_PEAK_G_WAVE_INSTS = 256 * 4 * 2.4 / 4
+
+
+def valu_roofline(kavg, ms_step, B):
+    """VALU issue utilisation from the latest committed rocprofv3 SQ_INSTS_VALU pass
+    (profiles/<tag>_pmc_valu.json, same 4096-proof batch): per kernel over its serial launch
+    time, and for the whole (pipelined) step.  None when no PMC summary is present."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_valu.json")))
+    if not files:
+        return None
+    pm = json.load(open(files[-1]))
+    ins = {k: v["SQ_INSTS_VALU"] for k, v in pm.items() if not k.startswith("_") and v.get("SQ_INSTS_VALU")}
+    scale = B / 4096.0   # the PMC pass ran 4096-proof batches
+    per = {}
+    for k, n in ins.items():
+        if kavg.get(k):
+            per[k] = round(n * scale / (kavg[k] * 1e-3) / 1e9 / VALU_PEAK_G_WAVE_INSTS, 3)
+    tot = sum(ins.values()) * scale
+    return {"unit": "G wave-instr/s", "peak": VALU_PEAK_G_WAVE_INSTS,
+            "step_achieved": round(tot / (ms_step * 1e-3) / 1e9, 1),
+            "step_frac": round(tot / (ms_step * 1e-3) / 1e9 / VALU_PEAK_G_WAVE_INSTS, 3),
+            "kernel_frac_serial": per, "source": os.path.relpath(files[-1], ROOT),
+            "note": "SQ_INSTS_VALU per step (all kernels) over the pipelined step time: the binding resource"}
 
 
 def log(*a):
@@ -164,6 +190,8 @@ def main():
     ap.add_argument("--lookups", type=int, default=0,
                     help="0: standard recursion circuit (C2); 2: + LookupGate/LookupTableGate with a 256-entry and a 2^16-entry table (C3 circuit)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL; the driver's multi-GPU runs) or gloo (rehearsing N ranks on fewer GPUs)")
     ap.add_argument("--quick", action="store_true", help="device-resident figure only (no ingest / PCIe / CPU legs)")
     args = ap.parse_args()
 
@@ -173,7 +201,9 @@ def main():
     import torch
     import torch.distributed as dist
     if world > 1:
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(args.dist_backend if torch.cuda.is_available() else "gloo")
+    # one rank per GPU; ranks beyond the visible GPUs (gloo rehearsal only) share devices
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     import p2v
 
@@ -212,7 +242,7 @@ def main():
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t
-        tmax = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tmax = torch.tensor([dt], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         if world > 1:
             dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         return float(tmax.item()), ktimes
@@ -266,7 +296,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
                          "traffic_bytes_per_launch": traffic_bytes, "algorithmic_bytes_per_launch": kb[dom] * B,
                          "note": "integer-VALU bound (Poseidon); HBM fraction reported as the metric asks"},
-            "valu": {"perms_per_proof": ppp, "perm_rate_G": round(value / world * ppp / 1e9, 3)},
+            "valu": {"perms_per_proof": ppp, "perm_rate_G": round(value / world * ppp / 1e9, 3),
+                     "issue": valu_roofline(kavg, dt / args.steps * 1e3, B) if not args.lookups else None},
             "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
             "verified_all": ok,
         }

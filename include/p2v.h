@@ -119,6 +119,15 @@ int  p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n,
 int  p2v_verify_batch(const p2v_circuit* c, const uint64_t* proofs, size_t n,
                       int8_t* results, int device);
 
+/* Single-process multi-GPU form of p2v_verify_batch: the batch (host memory,
+ * proof-major) is split into ndevices contiguous near-equal shards, shard i verified on
+ * devices[i] (a device may repeat) by its own host thread, stream and verifier, in chunks of
+ * at most `chunk` proofs (0: 16384) copied H2D per chunk.  Proofs are independent, so there is
+ * no cross-device traffic.  On failure returns the first failing shard's code and message.
+ * Replaces: map (verifyProof vkey) over a batch (Plonk/Verifier.hs:56-65) on N GPUs. */
+int  p2v_verify_batch_devices(const p2v_circuit* c, const uint64_t* proofs, size_t n, int8_t* results,
+                              const int* devices, int ndevices, size_t chunk);
+
 /* Per-launch timing of the last run (milliseconds, from HIP events on the run's stream):
  * out[k] for kernel k in the order named by p2v_kernel_names(). Returns count. */
 int  p2v_verifier_last_timings(const p2v_verifier* v, float* out, int max);

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -212,6 +213,16 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   d.o_zs = L.o_zs; d.o_pp = L.o_pp; d.o_quot = L.o_quot; d.o_lzs = L.o_lzs; d.o_zs_next = L.o_zs_next; d.o_lzs_next = L.o_lzs_next;
   d.n_this = L.n_this; d.n_next = L.n_next; d.ccaps = L.ccaps; d.final_poly = L.final_poly; d.pow = L.pow; d.q0 = L.q0; d.qstride = L.qstride;
   for (int t = 0; t < 4; t++) { d.leaf[t] = L.leaf[t]; d.path[t] = L.path[t]; }
+  {   // unit orders: most expensive tree first (stable), see DevCircuit::leaf_order
+    std::vector<std::pair<int64_t, int>> lc, mc;
+    for (int t = 0; t < d.T; t++) {
+      const int64_t len = t < 4 ? C.oracle_width[t] : (2ll << C.arities[t - 4]);
+      lc.push_back({-(len + 7) / 8, t});
+      mc.push_back({-(int64_t)(t < 4 ? C.depth0 : C.step_depth[t - 4]), t});
+    }
+    std::stable_sort(lc.begin(), lc.end()); std::stable_sort(mc.begin(), mc.end());
+    for (int k = 0; k < d.T; k++) { d.leaf_order[k] = (int8_t)lc[k].second; d.merkle_order[k] = (int8_t)mc[k].second; }
+  }
   for (int s = 0; s < d.S; s++) { d.step_evals[s] = L.step_evals[s]; d.step_path[s] = L.step_path[s]; d.arity[s] = C.arities[s]; d.step_depth[s] = C.step_depth[s]; }
   d.words = L.words;
   for (int i = 0; i < 4; i++) d.digest[i] = C.digest[i];
@@ -417,6 +428,43 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     HCK(hipStreamSynchronize(st));
     if (tm) for (int k = 0; k < kNumKernels; k++) { float ms = 0; if (hipEventElapsedTime(&ms, v->ev[2 * k], v->ev[2 * k + 1]) == hipSuccess) v->last_ms[k] = ms; }
   }
+  return P2V_OK;
+}
+
+int p2v_verify_batch_devices(const p2v_circuit* c, const uint64_t* proofs, size_t n, int8_t* results,
+                             const int* devices, int ndevices, size_t chunk) {
+  if (!c || !devices || ndevices <= 0 || (n && (!proofs || !results))) return fail(P2V_E_ARG, "null argument / no devices");
+  if (n == 0) return P2V_OK;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(P2V_E_NODEVICE, "no HIP device available: libp2v verifies on MI355X only (no CPU fallback)");
+  for (int i = 0; i < ndevices; i++)
+    if (devices[i] < 0 || devices[i] >= ndev) return fail(P2V_E_ARG, "bad device index " + std::to_string(devices[i]));
+  if (chunk == 0) chunk = 16384;
+  const size_t W = (size_t)c->c.L.words;
+  const int shards = (int)std::min<size_t>((size_t)ndevices, n);
+  std::vector<int> rcs(shards, P2V_OK);
+  std::vector<std::string> msgs(shards);
+  auto work = [&](int s) {
+    const size_t base = n / shards, extra = n % shards;   // p2v.shard_bounds
+    const size_t a = s * base + std::min<size_t>(s, extra), b = a + base + ((size_t)s < extra ? 1 : 0);
+    int rc = P2V_OK;
+    p2v_verifier* v = nullptr;
+    hipStream_t st = nullptr;
+    if (hipSetDevice(devices[s]) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
+      rc = fail(P2V_E_DEVICE, "stream creation on device " + std::to_string(devices[s]));
+    if (rc == P2V_OK) rc = p2v_verifier_create(c, devices[s], std::min(chunk, b - a), &v);
+    for (size_t i = a; rc == P2V_OK && i < b; i += chunk)
+      rc = p2v_verifier_run(v, proofs + i * W, std::min(chunk, b - i), results + i, nullptr, st, 0);
+    if (rc != P2V_OK) msgs[s] = g_err;   // g_err is thread-local: carry the message back
+    rcs[s] = rc;
+    p2v_verifier_free(v);
+    if (st) (void)hipStreamDestroy(st);
+  };
+  std::vector<std::thread> pool;
+  for (int s = 0; s < shards; s++) pool.emplace_back(work, s);
+  for (auto& t : pool) t.join();
+  for (int s = 0; s < shards; s++)
+    if (rcs[s] != P2V_OK) return fail(rcs[s], "shard " + std::to_string(s) + " (device " + std::to_string(devices[s]) + "): " + msgs[s]);
   return P2V_OK;
 }
 

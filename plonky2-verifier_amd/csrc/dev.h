@@ -18,6 +18,9 @@ struct DevCircuit {
   int32_t depth0, final_len;
   int32_t arity[P2V_MAX_STEPS], step_depth[P2V_MAX_STEPS], step_logn[P2V_MAX_STEPS];
   int32_t width[4];
+  // tree t of each unit position, most expensive first, so long waves dispatch first and short
+  // ones fill the tail: leaf hashing by sponge length, Merkle paths by depth
+  int8_t leaf_order[4 + P2V_MAX_STEPS], merkle_order[4 + P2V_MAX_STEPS];
   int32_t n_gates;                 // gates evaluated = min(#selector_indices, #gates)
   int32_t n_pp_terms, n_lookup_terms;
   int64_t alpha_base_gates;

@@ -44,8 +44,8 @@ extern "C" __global__ void __launch_bounds__(256) k_transpose(const uint64_t* __
 // ------------------------------------------------------------------------ helpers
 __device__ __forceinline__ void leaf_hash_unit(const DevCircuit& c, int unit, int lane) {
   const int NPB = c.B >> 6;
-  const int pb = unit % NPB, qt = unit / NPB;
-  const int q = qt / c.T, t = qt % c.T;
+  const int pb = unit % NPB, qt = unit / NPB;   // (position, query)-major: costly trees first
+  const int q = qt % c.Q, t = c.leaf_order[qt / c.Q];
   const int p = pb * 64 + lane;
   const int64_t base = c.q0 + (int64_t)q * c.qstride;
   int64_t off; int len;
@@ -284,8 +284,8 @@ extern "C" __global__ void __launch_bounds__(256) k_merkle(DevCircuit c) {
   const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int NPB = c.B >> 6;
   if (unit >= c.Q * c.T * NPB) return;
-  const int pb = unit % NPB, qt = unit / NPB;
-  const int q = qt / c.T, t = qt % c.T;
+  const int pb = unit % NPB, qt = unit / NPB;   // (position, query)-major: deepest paths first
+  const int q = qt % c.Q, t = c.merkle_order[qt / c.Q];
   const int p = pb * 64 + lane;
   const int64_t base = c.q0 + (int64_t)q * c.qstride;
   uint32_t idx = (uint32_t)chal(c, CH_QIDX(c) + q, p);

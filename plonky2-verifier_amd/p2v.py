@@ -112,6 +112,7 @@ def lib() -> ctypes.CDLL:
     L.p2v_verifier_free.restype = None
     L.p2v_verifier_run.argtypes = [vp, u64p, sz, i8p, u64p, vp, ctypes.c_uint32]
     L.p2v_verify_batch.argtypes = [vp, u64p, sz, i8p, ctypes.c_int]
+    L.p2v_verify_batch_devices.argtypes = [vp, u64p, sz, i8p, ctypes.POINTER(ctypes.c_int), ctypes.c_int, sz]
     L.p2v_verifier_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
     L.p2v_kernel_names.restype = ctypes.c_char_p
     L.p2v_last_error_message.restype = ctypes.c_char_p
@@ -306,6 +307,17 @@ def verify_proof_batch(vkey: VerifierCircuitData, proofs: Iterable[Union[ProofWi
 
 
 # ----------------------------------------------------------------------------- multi-GPU
+def verify_batch_devices(vkey: VerifierCircuitData, packed: np.ndarray, devices: Sequence[int], chunk: int = 0) -> np.ndarray:
+    """Single-process multi-GPU verification (p2v_verify_batch_devices): contiguous shards of
+    the packed batch, one per entry of `devices`, each on its own host thread; int8 statuses."""
+    packed = np.ascontiguousarray(packed, dtype=np.uint64)
+    n = packed.shape[0]
+    res = np.empty(n, dtype=np.int8)
+    devs = (ctypes.c_int * len(devices))(*devices)
+    _check(lib().p2v_verify_batch_devices(vkey.handle, packed.ctypes.data, n, res.ctypes.data, devs, len(devices), chunk))
+    return res
+
+
 def shard_bounds(n: int, world: int, rank: int):
     """Contiguous near-equal shard [start, end) of n proofs for `rank` of `world`.
     Proofs are independent (verifyProof has no cross-proof state), so a batch shards

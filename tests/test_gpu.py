@@ -135,6 +135,22 @@ def test_verify_proof_api(p2v):
     assert out == [True, False]
 
 
+def test_gpu_multi_device_entry_point(p2v):
+    """p2v_verify_batch_devices: shards on their own host threads / streams / verifiers (here
+    three shards on device 0), chunked, must equal the single-verifier statuses."""
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    pool = vk.pack_many([gc.proof(1, 1), gc.proof(1, 5, flags=2), gc.proof(1, 4, flags=1), gc.proof(2, 2)])
+    idx = np.random.default_rng(3).integers(0, 4, 701)
+    arr = np.ascontiguousarray(pool[idx])
+    want = p2v.BatchVerifier(vk, 0, len(idx)).run(arr)
+    assert sorted(set(want.tolist())) == [-3, 0, 1]
+    got = p2v.verify_batch_devices(vk, arr, [0, 0, 0], chunk=100)
+    assert np.array_equal(got, want)
+    with pytest.raises(p2v.P2VError):
+        p2v.verify_batch_devices(vk, arr, [0, 99])
+
+
 def test_gpu_c3_lookup_batch_full_size(p2v):
     """BASELINE configs[2] shape: 65 536 proofs of the lookup circuit (LookupGate +
     LookupTableGate, a 256-entry and a 2^16-entry table) at degree_bits 12 in one batch.

@@ -164,3 +164,6 @@ def test_verification_fails_loudly_without_gpu():
     with pytest.raises(p2v.P2VError) as e:
         p2v.verify_proof(vk, gc.proof(1, 1))
     assert e.value.code == -6   # P2V_E_NODEVICE: no CPU fallback
+    with pytest.raises(p2v.P2VError) as e:
+        p2v.verify_batch_devices(vk, vk.pack_many([gc.proof(1, 1)]), [0, 1])
+    assert e.value.code == -6
