@@ -13,8 +13,9 @@ collective: weak scaling); value = all proofs of all ranks / max-over-ranks time
 Workload: synthetic valid proofs from the degenerate-circuit prover (csrc/gen): standard
 recursion config (degree_bits 12, rate_bits 3, cap_height 4, 28 queries, arity 16, PoW 16,
 135 wires / 80 routed, 14-gate recursion gate set incl. Poseidon + CosetInterpolation),
-D distinct proofs per rank tiled into distinct HBM memory.  Every timed batch's results
-are checked (all must accept; a mutated sample must reject).
+D distinct proofs per rank tiled into distinct HBM memory, 1/16 of them corrupted (initial
+Merkle leaf -> -1, last step sibling -> -2).  Every timed batch's statuses are checked
+against the expected vector.
 """
 from __future__ import annotations
 
@@ -104,6 +105,30 @@ def kernel_bytes_model(info, trace_words):
     }
 
 
+def mutate_batch(tiled, info, every=16):
+    """Corrupt every `every`-th proof of the packed batch in place; returns the expected int8
+    statuses.  Alternately (a) the first leaf word of query 0's constants/sigmas tree (initial
+    Merkle check fails in round 0: status -1, Plonk/FRI.hs:108) and (b) the proof's last word,
+    a Merkle sibling of the last query's last FRI step (every earlier check passes: -2,
+    Plonk/FRI.hs:310).  Neither word is absorbed by the transcript, so nothing earlier
+    changes.  Values stay canonical (w + 1 mod p)."""
+    P = 0xFFFFFFFF00000001
+    W, Q = info.proof_words, info.num_query_rounds
+    depth0 = info.lde_bits - info.cap_height
+    qstride = sum(info.oracle_widths) + 4 * 4 * depth0
+    logn = info.lde_bits
+    for a in info.step_arity_bits:
+        logn -= a
+        qstride += (2 << a) + 4 * max(0, logn - info.cap_height)
+    q0 = W - Q * qstride   # query rounds are the layout's tail: [4 leaves | 4 paths | steps] each
+    expect = np.ones(tiled.shape[0], dtype=np.int8)
+    for k, i in enumerate(range(every // 2 - 1, tiled.shape[0], every)):
+        w = q0 if k % 2 == 0 else W - 1
+        tiled[i, w] = np.uint64((int(tiled[i, w]) + 1) % P)
+        expect[i] = -1 if k % 2 == 0 else -2
+    return expect
+
+
 def perms_per_proof(info, num_pis=4):
     """Poseidon permutations per proof (SURVEY.md §8d model; commentary/FRI.md:263-265)."""
     Q = info.num_query_rounds
@@ -162,7 +187,7 @@ def ingest_rate(vk, proofs, threads):
             "note": "host JSON->packed (template-guided scan; DOM reader for anything else)"}
 
 
-def h2d_rate(bv, tiled, B, steps=3):
+def h2d_rate(bv, tiled, B, expect, steps=3):
     """PCIe-inclusive: packed proofs in pinned host memory, H2D copy inside the timed run."""
     import torch
     host = torch.from_numpy(tiled.view(np.int64)).pin_memory()
@@ -172,7 +197,7 @@ def h2d_rate(bv, tiled, B, steps=3):
     for _ in range(steps):
         res = bv.run(arr)
     dt = (time.perf_counter() - t) / steps
-    assert bool((res == 1).all())
+    assert np.array_equal(res, expect)
     return {"value": round(B / dt, 1), "unit": "proofs/s", "ms_per_step": round(dt * 1e3, 3),
             "note": f"{B} proofs from pinned host memory per step, H2D {tiled.nbytes / 1e6:.0f} MB + verify + D2H, one batch at a time"}
 
@@ -216,8 +241,12 @@ def main():
     packed = vk.pack_many(proofs)
     B = args.batch
     tiled = np.ascontiguousarray(packed[np.arange(B) % len(proofs)])
+    # 1/16 of the batch is corrupted: the GPU does the same work for them, and
+    # the statuses of every timed batch are checked against the expected vector
+    expect = mutate_batch(tiled, info)
     dev = torch.device("cuda", local)
     d_proofs = torch.from_numpy(tiled.view(np.int64)).to(dev)
+    d_expect = torch.from_numpy(expect).to(dev)
     nv = max(1, args.inflight)
     d_res = [torch.empty(B, dtype=torch.int8, device=dev) for _ in range(nv)]
     bvs = [p2v.BatchVerifier(vk, local, B) for _ in range(nv)]
@@ -250,15 +279,15 @@ def main():
     for i in range(args.warmup):
         bvs[i % nv].run_device(d_proofs.data_ptr(), B, d_res[i % nv].data_ptr(), stream=streams[i % nv].cuda_stream, sync=False)
     torch.cuda.synchronize(dev)
-    assert all(bool((r == 1).all()) for r in d_res[:max(1, min(nv, args.warmup))]), "generated batch did not verify on the GPU"
+    assert all(bool((r == d_expect).all()) for r in d_res[:max(1, min(nv, args.warmup))]), "batch statuses differ from the expected ones"
     # serial pass: per-kernel durations (HIP events recorded on the run's streams inside libp2v)
     dt_serial, ktimes = timed(args.steps, False)
-    ok = bool((d_res[0] == 1).all())
+    ok = bool((d_res[0] == d_expect).all())
     if nv > 1:
         for r in d_res:
             r.zero_()
         dt, _ = timed(args.steps, True)
-        ok = ok and all(bool((r == 1).all()) for r in d_res[:min(nv, args.steps)])
+        ok = ok and all(bool((r == d_expect).all()) for r in d_res[:min(nv, args.steps)])
     else:
         dt = dt_serial
     total = B * args.steps * world
@@ -287,7 +316,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "u64 (Goldilocks mod-p integer)", "data": "synthetic",
             "config": {"workload": f"{'C3' if args.lookups else 'C2'}: {B} std-config Plonky2 proofs per GPU per step (degree_bits {info.degree_bits}, "
                                    f"28 FRI queries, arity 16, deg-2 ext{', lookups: 256 + 65536-entry tables' if args.lookups > 1 else (', lookups' if args.lookups else '')}), "
-                                   f"{len(proofs)} distinct tiled, device-resident",
+                                   f"{len(proofs)} distinct tiled, 1/16 corrupted, device-resident",
                        "global_batch": B * world, "degree_bits": info.degree_bits, "parallelism": f"proof-sharded x{world}",
                        "inflight": nv},
             "serial": {"value": round(total / dt_serial, 1), "ms_per_step": round(dt_serial / args.steps * 1e3, 4),
@@ -303,7 +332,7 @@ def main():
         }
         if world == 1 and not args.quick:
             out["ingest"] = ingest_rate(vk, proofs, threads)
-            out["h2d_end_to_end"] = h2d_rate(bvs[0], tiled, B)
+            out["h2d_end_to_end"] = h2d_rate(bvs[0], tiled, B, expect)
         if world == 1 and not args.no_cpu_baseline and not args.quick:
             out["cpu_baseline"] = cpu_baseline(gc, proofs, threads)
         print(json.dumps(out), flush=True)

@@ -67,28 +67,35 @@ __device__ __forceinline__ void qrow(const uint64_t (&X)[4][3], uint64_t& al, ui
   }
 }
 
-// x <- M x + k (k = the next round's constants of this lane's rows, split into halves)
-__device__ __forceinline__ void mds(uint64_t x[3], int t, const uint64_t kl[3], const uint64_t kh[3]) {
+// (al, ah)[m] = rows 3t+m of M x + k, unreduced (k = the next round's constants of this lane's
+// rows, split into halves)
+__device__ __forceinline__ void mds_acc(const uint64_t x[3], int t, const uint64_t kl[3], const uint64_t kh[3],
+                                        uint64_t al[3], uint64_t ah[3]) {
   uint64_t X[4][3];
 #pragma unroll
   for (int k = 0; k < 3; k++) { X[0][k] = x[k]; X[1][k] = rot64<1>(x[k]); X[2][k] = rot64<2>(x[k]); X[3][k] = rot64<3>(x[k]); }
   const uint64_t c00 = t == 0 ? 25 : 17;   // circ[0] (+ diag[0] on row 0)
-  uint64_t al0 = kl[0], ah0 = kh[0], al1 = kl[1], ah1 = kh[1], al2 = kl[2], ah2 = kh[2];
-  qrow<0, 0>(X, al0, ah0, c00);
-  qrow<1, 0>(X, al1, ah1, c00);
-  qrow<2, 0>(X, al2, ah2, c00);
-  x[0] = p2::mds_reduce(al0, ah0);
-  x[1] = p2::mds_reduce(al1, ah1);
-  x[2] = p2::mds_reduce(al2, ah2);
+#pragma unroll
+  for (int m = 0; m < 3; m++) { al[m] = kl[m]; ah[m] = kh[m]; }
+  qrow<0, 0>(X, al[0], ah[0], c00);
+  qrow<1, 0>(X, al[1], ah[1], c00);
+  qrow<2, 0>(X, al[2], ah[2], c00);
 }
 
-// the quad's permutation; x = this lane's three words (inputs < 2^64, outputs canonical)
+// the quad's permutation; x = this lane's three words (inputs < 2^64, outputs canonical).
+// Partial rounds take the S-box off the critical path: the MDS runs on the state with word 0
+// zeroed while lane 0's S-box chain is in flight, then sbox(word 0), broadcast from lane 0,
+// is added with column 0 of M (M[3t+m][0], per lane).
 __device__ __forceinline__ void permute(uint64_t x[3], int t) {
   {
     const uint64_t* R = p2::c_round_constants + 3 * t;
 #pragma unroll
     for (int k = 0; k < 3; k++) x[k] = p2::add_nc(x[k], R[k]);
   }
+  // M[i][0] = circ[(12 - i) % 12] (+ 8 for i = 0), rows i = 3t .. 3t+2 (Hash/Constants.hs:19-25)
+  const uint32_t col0[3] = {t == 0 ? 25u : t == 1 ? 18u : t == 2 ? 13u : 16u,
+                            t == 0 ? 20u : t == 1 ? 39u : t == 2 ? 28u : 41u,
+                            t == 0 ? 34u : t == 1 ? 13u : t == 2 ? 2u : 15u};
   uint64_t kl[3], kh[3], nkl[3], nkh[3];
   lane_rc(1, t, nkl, nkh);
 #pragma unroll 1
@@ -96,15 +103,24 @@ __device__ __forceinline__ void permute(uint64_t x[3], int t) {
 #pragma unroll
     for (int k = 0; k < 3; k++) { kl[k] = nkl[k]; kh[k] = nkh[k]; }
     lane_rc(r + 2 <= 30 ? r + 2 : 30, t, nkl, nkh);   // row 30 of the split table is zero
-    const bool full = r < 4 || r >= 26;
-    if (full) {
+    uint64_t al[3], ah[3];
+    if (r < 4 || r >= 26) {
 #pragma unroll
       for (int k = 0; k < 3; k++) x[k] = p2::sbox(x[k]);
+      mds_acc(x, t, kl, kh, al, ah);
     } else {
-      const uint64_t s = p2::sbox(x[0]);   // computed by every lane, kept by lane 0 (word 0)
-      x[0] = t == 0 ? s : x[0];
+      const uint64_t w0 = x[0];
+      x[0] = t == 0 ? 0 : w0;
+      mds_acc(x, t, kl, kh, al, ah);           // independent of the S-box below
+      const uint64_t s = bcast64(p2::sbox(w0), 0);
+#pragma unroll
+      for (int m = 0; m < 3; m++) {
+        al[m] += (uint64_t)(uint32_t)s * col0[m];
+        ah[m] += (s >> 32) * col0[m];
+      }
     }
-    mds(x, t, kl, kh);
+#pragma unroll
+    for (int m = 0; m < 3; m++) x[m] = p2::mds_reduce(al[m], ah[m]);
   }
 #pragma unroll
   for (int k = 0; k < 3; k++) x[k] = gl::canon(x[k]);

@@ -175,3 +175,25 @@ def test_gpu_c3_lookup_batch_full_size(p2v):
         lanes = np.nonzero(idx == k)[0]
         for lane in (lanes[0], lanes[-1]):
             assert np.array_equal(tr[lane], otr), (k, lane)
+
+
+@pytest.mark.parametrize("nb,pis,lk,q,pw", [
+    (10, 0, 0, 28, 16),    # no public inputs: PI hash = sponge [] = zero digest (Hash/Sponge.hs:26-31)
+    (13, 9, 0, 28, 16),    # deeper trees (LDE 2^16), two PI sponge blocks
+    (12, 4, 1, 20, 8),     # lookups, 20 queries, 8 PoW bits
+    (7, 17, 0, 12, 0),     # odd degree (FRI steps 4 + final), 3 PI blocks, no proof of work
+])
+def test_gpu_circuit_shape_sweep_vs_oracle(p2v, nb, pis, lk, q, pw):
+    O = oracle()
+    gc = gen_circuit(nb, pis, lk, 1, q, pw)
+    kinds = [(1, 1, 0), (2, 3, 0), (1, 4, 1), (1, 5, 2), (1, 6, 4)][: 3 if nb > 12 else 5]
+    cases = [gc.proof(w, s, flags=f) for w, s, f in kinds]
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    res, tr = p2v.BatchVerifier(vk, 0, len(cases)).run(vk.pack_many(cases), trace=True)
+    sts = []
+    for i, proof in enumerate(cases):
+        st, otr = O.verify_json(gc.common, gc.vkey, proof, trace=True)
+        sts.append(st)
+        assert res[i] == st, i
+        assert np.array_equal(tr[i], otr), (i, np.nonzero(tr[i] != otr)[0][:10])
+    assert sts == [1, 1, -3, 0, 0][: len(cases)]

@@ -167,3 +167,45 @@ def test_verification_fails_loudly_without_gpu():
     with pytest.raises(p2v.P2VError) as e:
         p2v.verify_batch_devices(vk, vk.pack_many([gc.proof(1, 1)]), [0, 1])
     assert e.value.code == -6
+
+
+def test_bench_mutation_offsets_hit_the_intended_words():
+    """bench.py corrupts 1/16 of each batch at two packed offsets it derives from the layout;
+    check they are query 0's first constants/sigmas leaf word and the last query's last
+    step sibling word (so the expected statuses -1 / -2 hold)."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    p2v = p2v_module()
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    text = gc.proof(2, 2)
+    packed = vk.pack_many([text] * 32)
+    orig = packed.copy()
+    expect = bench.mutate_batch(packed, vk.info)
+    assert list(np.flatnonzero(expect != 1)) == [7, 23] and list(expect[[7, 23]]) == [-1, -2]
+    d = json.loads(text)["proof"]["opening_proof"]["query_round_proofs"]
+    leaf = d[0]["initial_trees_proof"]["evals_proofs"][0][0]
+    sib = d[-1]["steps"][-1]["merkle_proof"]["siblings"][-1]["elements"][-1]
+    (w7,) = np.flatnonzero(packed[7] != orig[7])
+    (w23,) = np.flatnonzero(packed[23] != orig[23])
+    assert list(orig[7, w7:w7 + len(leaf)]) == [x % P for x in leaf]
+    assert w23 == vk.info.proof_words - 1 and int(orig[23, w23]) == sib % P
+    from support import oracle
+    O = oracle()
+
+    def corrupt(fn):
+        dd = json.loads(text)
+        fn(dd["proof"]["opening_proof"]["query_round_proofs"])
+        return json.dumps(dd).encode()
+
+    def f_leaf(q):
+        q[0]["initial_trees_proof"]["evals_proofs"][0][0][0] = (leaf[0] + 1) % P
+
+    def f_sib(q):
+        q[-1]["steps"][-1]["merkle_proof"]["siblings"][-1]["elements"][-1] = (sib + 1) % P
+    assert O.verify_json(gc.common, gc.vkey, corrupt(f_leaf)) == -1
+    assert O.verify_json(gc.common, gc.vkey, corrupt(f_sib)) == -2
+    assert np.array_equal(vk.pack(corrupt(f_leaf)), packed[7])
+    assert np.array_equal(vk.pack(corrupt(f_sib)), packed[23])
