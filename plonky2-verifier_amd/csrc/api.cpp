@@ -70,6 +70,7 @@ struct p2v_verifier {
   bool timed = false;
   int transcript_mode = 0;          // 0 auto, 1 row, 2 quad (env P2V_TRANSCRIPT)
   int quad_min_batch = 2048;        // auto: quad form from this batch size on
+  bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
 };
 
 extern "C" {
@@ -197,6 +198,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   auto* v = new p2v_verifier();
   v->circ = pc; v->device = device; v->max_batch = max_batch;
   v->Bmax = (max_batch + 63) / 64 * 64;
+  if (const char* ss = getenv("P2V_SINGLE_STREAM")) v->single_stream = ss[0] == '1';
   if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : 0;
   DevCircuit& d = v->dc;
   memset(&d, 0, sizeof d);
@@ -374,7 +376,7 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   if (trace) dtrace = (flags & P2V_FLAG_RESULT_DEVICE) ? trace : (uint64_t*)v->trace.p;
   const int NPB = d.B / 64;
   const bool tm = v->timed;
-  hipStream_t sd = v->side;
+  hipStream_t sd = v->single_stream ? st : v->side;
 #define T0(k, s_) do { if (tm) HCK(hipEventRecord(v->ev[2 * (k)], s_)); } while (0)
 #define T1(k, s_) do { if (tm) HCK(hipEventRecord(v->ev[2 * (k) + 1], s_)); } while (0)
   T0(0, st);
@@ -395,8 +397,10 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   T1(1, st);
   // phase 2: Merkle paths on the main stream; FRI queries and the vanishing kernel (few,
   // long-latency waves) on the side stream, concurrently
-  HCK(hipEventRecord(v->dep_p1, st));
-  HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));
+  if (sd != st) {
+    HCK(hipEventRecord(v->dep_p1, st));
+    HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));
+  }
   T0(7, sd);
   if (d.n_lut_pieces > 0) k_lut<<<(d.r * d.n_lut_pieces * NPB + 3) / 4, 256, 0, sd>>>(d);
   T1(7, sd);
@@ -409,11 +413,11 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   T0(3, sd);
   k_fri<<<(d.Q * NPB + 3) / 4, 256, 0, sd>>>(d);
   T1(3, sd);
-  HCK(hipEventRecord(v->dep_side, sd));
+  if (sd != st) HCK(hipEventRecord(v->dep_side, sd));
   T0(2, st);
   k_merkle<<<(leaf_units + 3) / 4, 256, 0, st>>>(d);
   T1(2, st);
-  HCK(hipStreamWaitEvent(st, v->dep_side, 0));
+  if (sd != st) HCK(hipStreamWaitEvent(st, v->dep_side, 0));
   T0(5, st);
   k_status<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(d, dres, dtrace, C.trace_words);
   T1(5, st);
