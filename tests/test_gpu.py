@@ -197,3 +197,17 @@ def test_gpu_circuit_shape_sweep_vs_oracle(p2v, nb, pis, lk, q, pw):
         assert res[i] == st, i
         assert np.array_equal(tr[i], otr), (i, np.nonzero(tr[i] != otr)[0][:10])
     assert sts == [1, 1, -3, 0, 0][: len(cases)]
+
+
+def test_gpu_c_abi_host_example_matches_golden(p2v, tmp_path):
+    """examples/p2v_verify.c (plain C over include/p2v.h) on the golden fixtures, one GPU
+    and the multi-device entry (--devices 1 shards nothing; the statuses must not change)."""
+    import subprocess
+    from test_host import _c_host_args
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "plonky2-verifier_amd", "p2v_verify")
+    exp = [c for c in json.load(open(os.path.join(GOLDEN, "expected.json")))["cases"] if c["circuit"] == "circuit_n6_lk0_pow16"]
+    args = _c_host_args(tmp_path, "circuit_n6_lk0_pow16", [c["name"] for c in exp])
+    for extra in ([], ["--devices", "1"]):
+        out = subprocess.run([exe] + extra + args, capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stderr
+        assert [int(ln.split()[1]) for ln in out.stdout.splitlines()] == [c["status"] for c in exp]

@@ -209,3 +209,35 @@ def test_bench_mutation_offsets_hit_the_intended_words():
     assert O.verify_json(gc.common, gc.vkey, corrupt(f_sib)) == -2
     assert np.array_equal(vk.pack(corrupt(f_leaf)), packed[7])
     assert np.array_equal(vk.pack(corrupt(f_sib)), packed[23])
+
+
+def _c_host_args(tmp_path, circuit, names):
+    """gunzip a golden circuit + proofs into tmp_path; return the p2v_verify argument list."""
+    paths = []
+    for n in [circuit + "_common", circuit + "_vkey"] + [x + "_proof" for x in names]:
+        p = tmp_path / (n + ".json")
+        with gzip.open(os.path.join(GOLDEN, n + ".json.gz"), "rb") as f:
+            p.write_bytes(f.read())
+        paths.append(str(p))
+    return paths
+
+
+def test_c_abi_host_example_packs_and_fails_loudly_without_gpu(tmp_path):
+    """examples/p2v_verify.c: a plain-C host over include/p2v.h (no Python in the path)."""
+    import subprocess
+    exe = os.path.join(ROOT, "plonky2-verifier_amd", "p2v_verify")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "plonky2-verifier_amd"), "p2v_verify"])
+    p2v = p2v_module()
+    args = _c_host_args(tmp_path, "circuit_n6_lk0_pow16", ["std_valid_a", "std_leaf"])
+    out = subprocess.run([exe, "--pack-only"] + args, capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    vk = p2v.VerifierCircuitData.from_json(open(args[0], "rb").read(), open(args[1], "rb").read())
+    assert [ln.split()[1] for ln in out.stdout.splitlines()] == [str(vk.info.proof_words)] * 2
+    bad = tmp_path / "bad.json"
+    bad.write_bytes(b"{")
+    assert subprocess.run([exe, "--pack-only", args[0], args[1], str(bad)], capture_output=True).returncode == 4
+    assert subprocess.run([exe, args[1], args[0], str(bad)], capture_output=True).returncode == 3
+    if p2v.device_count() == 0:
+        out = subprocess.run([exe] + args, capture_output=True, text=True)
+        assert out.returncode == 5 and "no HIP device" in out.stderr
