@@ -101,6 +101,10 @@ int  p2v_pack_proofs_json(const p2v_circuit* c, const char* const* jsons, const 
 #define P2V_FLAG_INPUT_DEVICE  1u  /* `proofs` is a device pointer on the verifier's device  */
 #define P2V_FLAG_RESULT_DEVICE 2u  /* `results` (and trace) are device pointers              */
 #define P2V_FLAG_NO_SYNC       4u  /* do not synchronise the stream before returning          */
+#define P2V_FLAG_UNIT_FILTERS  8u  /* parity mode: every gate filter and lookup selector := 1, so the
+                                      trace's combined values C_i expose every constraint program
+                                      (the oracle's or_verify full_trace bit 1); statuses are then
+                                      meaningless.  Tests only. */
 
 int  p2v_device_count(void);
 

@@ -502,6 +502,7 @@ typedef struct {
   F *betas, *gammas, *alphas; ldelta_t* deltas; int ndeltas;
   E zeta;
   E fri_alpha; E* fri_betas; int nfri_betas; F pow_response; long* query_idx; int nquery;
+  int unit_filters;   /* parity mode (or_verify full_trace bit 1): gate filters and lookup selectors := 1 */
 } chal_t;
 
 /* toFriOpenings, Challenge/FRI.hs:46-61 */
@@ -807,7 +808,7 @@ static void gate_constraints(const gate_t* g, const evars_t* V, clist* out) {
  * Plonk/Lookups.hs:45-132 */
 static void eval_lookup_equations(const circuit_t* C, const constcols_t* cc, const proof_t* P, const chal_t* ch, clist* out) {
   int nlp = C->nlp;
-#define SEL(idx) ((idx) < cc->nlsel ? cc->lsel[(idx)] : (fail(P2V_ERR_SHAPE, "Prelude.!!: index too large (lookup selector)"), E0()))
+#define SEL(idx) ((idx) < cc->nlsel ? (ch->unit_filters ? Eb(1) : cc->lsel[(idx)]) : (fail(P2V_ERR_SHAPE, "Prelude.!!: index too large (lookup selector)"), E0()))
   int npairs = P->n_lzs < P->n_lzs_next ? P->n_lzs : P->n_lzs_next;   /* zip */
   if (nlp <= 0) fail(P2V_ERR_CIRCUIT, "partition: non-positive lookup chunk");
   int nchunks = (npairs + nlp - 1) / nlp;
@@ -930,7 +931,7 @@ static void eval_all_constraints(arena* m, const circuit_t* C, const proof_t* P,
   for (int g = 0; g < ng; g++) {
     int grp = C->sel_idx[g];
     if (grp < 0 || grp >= cc.ngsel) fail(P2V_ERR_CIRCUIT, "Prelude.!!: index too large (selector column)");
-    E s = eval_gate_selector_poly(C, cc.gsel[grp], g);
+    E s = ch->unit_filters ? Eb(1) : eval_gate_selector_poly(C, cc.gsel[grp], g);
     clist cons = {0}; cons.m = m;
     gate_constraints(&C->gates[g], &V, &cons);
     for (int k = 0; k < cons.n; k++) {
@@ -1095,6 +1096,7 @@ __attribute__((noinline)) static int verify_body(const circuit_t* C, const proof
   int status;
   chal_t ch; memset(&ch, 0, sizeof ch);
   proof_challenges(m_, C, P, &ch);
+  ch.unit_filters = (full_trace & 2) != 0;
   int r = C->r, Q = C->nqueries;
   int arities[64]; int nsteps = expand_strategy(C, arities);
   long o_pi = 0, o_b = 4, o_g = o_b + r, o_a = o_g + r, o_d = o_a + r, o_z = o_d + 4 * r, o_fa = o_z + 2, o_fb = o_fa + 2,
@@ -1194,7 +1196,9 @@ or_proof* or_proof_load(const char* proof, size_t plen) {
 void or_proof_free(or_proof* p) { if (p) { afree(&p->p.mem); free(p); } }
 
 /* status of verifyProof; trace (optional) gets P2V_TRACE_WORDS(r,S,Q,L) words.
- * full_trace != 0 computes every trace value even past a deciding failure. */
+ * full_trace bit 0 computes every trace value even past a deciding failure; bit 1 sets every
+ * gate filter and lookup selector to 1 (parity mode: exposes every constraint program in the
+ * combined values C_i of the trace; the status is then meaningless). */
 int or_verify(const or_circuit* c, const or_proof* p, uint64_t* trace, int full_trace) {
   int s = verify_impl(&c->c, &p->p, trace, full_trace);
   if (s < 0) snprintf(g_last, sizeof g_last, "%s", g_msg);

@@ -364,6 +364,7 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   const Circuit& C = v->circ->c;
   DevCircuit d = v->dc;
   d.n = (int)n;
+  d.unit_filters = (flags & P2V_FLAG_UNIT_FILTERS) ? 1 : 0;
   d.B = (int)((n + 63) / 64 * 64);
   const int64_t words = C.L.words;
   const uint64_t* src = proofs;

@@ -22,6 +22,7 @@ struct DevCircuit {
   // ones fill the tail: leaf hashing by sponge length, Merkle paths by depth
   int8_t leaf_order[4 + P2V_MAX_STEPS], merkle_order[4 + P2V_MAX_STEPS];
   int32_t n_gates;                 // gates evaluated = min(#selector_indices, #gates)
+  int32_t unit_filters;            // P2V_FLAG_UNIT_FILTERS (parity mode)
   int32_t n_pp_terms, n_lookup_terms;
   int64_t alpha_base_gates;
   // packed layout (u64 word offsets)

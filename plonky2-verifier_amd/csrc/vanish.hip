@@ -414,7 +414,7 @@ __device__ void item_lookup(const DevCircuit& c, Acc& T, int j, int p) {
   const int nclu = (nlu + lu_degree - 1) / lu_degree, nclut = (nlut + lut_degree - 1) / lut_degree, ncm = (slots3 + lut_degree - 1) / lut_degree;
   int nz = nclu < nclut ? nclu : nclut; nz = nz < ncm ? nz : ncm; nz = nz < nsldc ? nz : nsldc;
   const int64_t ls = c.o_const + 2 * (int64_t)c.ngroups;   // lookup selectors
-  auto sel = [&](int k) { return lde(c, ls + 2 * k, p); };
+  auto sel = [&](int k) { return c.unit_filters ? gl::eb(1) : lde(c, ls + 2 * k, p); };
   auto wv = [&](int t) { return lde(c, c.o_wires + 2 * (int64_t)t, p); };
   const uint64_t dA = chal(c, CH_DELTA(c) + 4 * j, p), dB = chal(c, CH_DELTA(c) + 4 * j + 1, p);
   const uint64_t dal = chal(c, CH_DELTA(c) + 4 * j + 2, p), dde = chal(c, CH_DELTA(c) + 4 * j + 3, p);
@@ -500,6 +500,7 @@ __device__ void vanish_item(const DevCircuit& c, int it, int p) {
     const E unused = gl::eb(0xFFFFFFFFULL);
     E s = c.ngroups > 1 ? gl::esub(unused, x) : one;   // Gate/Selector.hs:83-89
     for (int j = c.grp_start[grp]; j < c.grp_end[grp]; j++) if (j != a) s = gl::emul(s, gl::esub(gl::eb((uint64_t)j), x));
+    if (c.unit_filters) s = one;
     Vars V{&c, p};
     eval_gate(c, V, T, a, b);
 #pragma unroll

@@ -58,6 +58,7 @@ E_OK, E_PARSE, E_CIRCUIT, E_SHAPE, E_ARG, E_DEVICE, E_NODEVICE = 0, -1, -2, -3, 
 FLAG_INPUT_DEVICE = 1
 FLAG_RESULT_DEVICE = 2
 FLAG_NO_SYNC = 4
+FLAG_UNIT_FILTERS = 8   # parity mode (tests only): every gate filter / lookup selector := 1
 
 
 class P2VError(RuntimeError):
@@ -240,14 +241,15 @@ class BatchVerifier:
         _check(lib().p2v_verifier_create(circuit.handle, device, max_batch, ctypes.byref(h)))
         self._h = h
 
-    def run(self, proofs: np.ndarray, trace: bool = False):
-        """proofs: uint64 [n, proof_words] host array.  Returns int8 statuses (and trace)."""
+    def run(self, proofs: np.ndarray, trace: bool = False, unit_filters: bool = False):
+        """proofs: uint64 [n, proof_words] host array.  Returns int8 statuses (and trace).
+        unit_filters: parity mode (P2V_FLAG_UNIT_FILTERS), statuses meaningless."""
         proofs = np.ascontiguousarray(proofs, dtype=np.uint64)
         n = proofs.shape[0]
         res = np.empty(n, dtype=np.int8)
         tr = np.empty((n, self.circuit.info.trace_words), dtype=np.uint64) if trace else None
         _check(lib().p2v_verifier_run(self._h, proofs.ctypes.data, n, res.ctypes.data,
-                                      tr.ctypes.data if trace else None, None, 0))
+                                      tr.ctypes.data if trace else None, None, FLAG_UNIT_FILTERS if unit_filters else 0))
         return (res, tr) if trace else res
 
     def run_device(self, proofs_ptr: int, n: int, results_ptr: int, stream: int = 0, trace_ptr: int = 0,

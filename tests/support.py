@@ -77,19 +77,19 @@ class Oracle:
             raise ValueError(self.L.or_last_error().decode())
         return h
 
-    def verify(self, circ, proof, trace=False, full=True):
+    def verify(self, circ, proof, trace=False, full=True, unit_filters=False):
         if trace:
             tw = self.L.or_trace_words(circ)
             tr = np.zeros(tw, dtype=np.uint64)
-            st = self.L.or_verify(circ, proof, tr.ctypes.data, 1 if full else 0)
+            st = self.L.or_verify(circ, proof, tr.ctypes.data, (1 if full else 0) | (2 if unit_filters else 0))
             return st, tr
         return self.L.or_verify(circ, proof, None, 0)
 
-    def verify_json(self, common: bytes, vkey: bytes, proof: bytes, trace=False):
+    def verify_json(self, common: bytes, vkey: bytes, proof: bytes, trace=False, unit_filters=False):
         c = self.circuit(common, vkey)
         p = self.proof(proof)
         try:
-            return self.verify(c, p, trace=trace)
+            return self.verify(c, p, trace=trace, unit_filters=unit_filters)
         finally:
             self.L.or_proof_free(p)
             self.L.or_circuit_free(c)

@@ -211,3 +211,24 @@ def test_gpu_c_abi_host_example_matches_golden(p2v, tmp_path):
         out = subprocess.run([exe] + extra + args, capture_output=True, text=True, timeout=120)
         assert out.returncode == 0, out.stderr
         assert [int(ln.split()[1]) for ln in out.stdout.splitlines()] == [c["status"] for c in exp]
+
+
+@pytest.mark.parametrize("nb,lk", [(6, 0), (6, 1), (6, 2), (8, 0), (12, 1)])
+def test_gpu_constraint_programs_vs_oracle_unit_filters(p2v, nb, lk):
+    """The generator's circuits have every gate filter and lookup selector 0 at zeta (valid
+    proofs need a satisfied identity), so the statuses and C_i alone would not see a wrong
+    gate program.  In parity mode (P2V_FLAG_UNIT_FILTERS / oracle full_trace bit 1) every
+    filter is 1: C_i(zeta) then carries the alpha-combined vertical sum of all 14 gate kinds'
+    constraints and every lookup term, and must equal the oracle's word for word."""
+    O = oracle()
+    gc = gen_circuit(nb, 4, lk)
+    cases = [gc.proof(1, 1), gc.proof(2, 7)]
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    _, tr = p2v.BatchVerifier(vk, 0, len(cases)).run(vk.pack_many(cases), trace=True, unit_filters=True)
+    _, tr0 = p2v.BatchVerifier(vk, 0, len(cases)).run(vk.pack_many(cases), trace=True)
+    r, S, Q = vk.info.num_challenges, vk.info.num_fri_steps, vk.info.num_query_rounds
+    o_c = 4 + 3 * r + 4 * r + 4 + 2 * S + 1 + Q   # off_combined (include/p2v.h)
+    for i, proof in enumerate(cases):
+        _, otr = O.verify_json(gc.common, gc.vkey, proof, trace=True, unit_filters=True)
+        assert np.array_equal(tr[i], otr), (i, np.nonzero(tr[i] != otr)[0][:10])
+        assert not np.array_equal(tr[i][o_c:o_c + 2 * r], tr0[i][o_c:o_c + 2 * r])   # the mode is live
