@@ -113,9 +113,12 @@ int  p2v_device_count(void);
 int  p2v_verifier_create(const p2v_circuit* c, int device, size_t max_batch, p2v_verifier** out);
 void p2v_verifier_free(p2v_verifier* v);
 
-/* Verify n packed proofs (n * proof_words u64, proof-major).  results[i] gets the status
- * of proof i.  trace (optional, may be NULL) receives n * trace_words u64 of intermediates
- * for parity checks.  stream: a hipStream_t cast to void* (NULL = the default stream). */
+/* Verify n packed proofs (n * proof_words u64, proof-major, each word a canonical field
+ * element < p as p2v_pack_proof_json writes it).  results[i] gets the status of proof i.
+ * trace (optional, may be NULL) receives n * trace_words u64 of intermediates for parity
+ * checks.  stream: a hipStream_t cast to void* (NULL = the default stream).  A verifier is
+ * one workspace: one run at a time per verifier (use one verifier per concurrent stream);
+ * circuits are read-only and may be shared. */
 int  p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n,
                       int8_t* results, uint64_t* trace, void* stream, uint32_t flags);
 
