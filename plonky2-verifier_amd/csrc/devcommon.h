@@ -63,47 +63,4 @@ __device__ __forceinline__ E epow_u(E x, uint32_t e) {   // uniform small expone
 }
 __device__ __forceinline__ E epow2n(E x, int n) { for (int i = 0; i < n; i++) x = gl::emul(x, x); return x; }
 
-// ---------------------------------------------------------------- state word access
-// uniform index into the 12-word register state (scalar branch, no scratch)
-__device__ __forceinline__ void st_set(uint64_t s[12], int i, uint64_t x) {
-  switch (i) {
-    case 0: s[0] = x; break; case 1: s[1] = x; break; case 2: s[2] = x; break; case 3: s[3] = x; break;
-    case 4: s[4] = x; break; case 5: s[5] = x; break; case 6: s[6] = x; break; case 7: s[7] = x; break;
-    default: break;
-  }
-}
-__device__ __forceinline__ uint64_t st_get(const uint64_t s[12], int i) {
-  switch (i) {
-    case 0: return s[0]; case 1: return s[1]; case 2: return s[2]; case 3: return s[3];
-    case 4: return s[4]; case 5: return s[5]; case 6: return s[6]; default: return s[7];
-  }
-}
-
-// Fiat–Shamir duplex in overwrite mode (Challenge/Pure.hs:27-107).  Buffered inputs are
-// written straight into the rate part of the state: nothing reads those words before the
-// duplex that would overwrite them, so permute(state) == duplex inp old.
-struct Duplex {
-  uint64_t s[12];
-  int nbuf;      // inputs buffered since the last duplex (uniform)
-  int outpos;    // next output word while squeezing (uniform), -1 = exhausted
-  bool absorbing;
-  __device__ __forceinline__ void init() {
-#pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = 0;
-    nbuf = 0; outpos = -1; absorbing = true;
-  }
-  __device__ __forceinline__ void absorb(uint64_t x) {
-    if (!absorbing) { absorbing = true; nbuf = 0; }
-    if (nbuf == 8) { p2::permute(s); nbuf = 0; }
-    st_set(s, nbuf, x);
-    nbuf++;
-  }
-  __device__ __forceinline__ uint64_t squeeze() {
-    if (absorbing || outpos < 0) { p2::permute(s); absorbing = false; outpos = 7; }
-    uint64_t v = st_get(s, outpos);
-    outpos--;
-    return v;
-  }
-};
-
 }  // namespace p2d
