@@ -187,6 +187,26 @@ def ingest_rate(vk, proofs, threads):
             "note": "host JSON->packed (template-guided scan; DOM reader for anything else)"}
 
 
+def json_rate(bv, proofs, B, steps=3):
+    """End to end from JSON: B proof texts (the distinct ones tiled) in pinned host memory,
+    copied to the device and packed there (p2v_verifier_run_json), then verified; one batch
+    at a time.  Reported next to the host packer's rate, never as the bench value."""
+    import torch
+    texts = [bytes(proofs[i % len(proofs)]) for i in range(B)]
+    offs = np.zeros(B + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(t) for t in texts])
+    blob = torch.from_numpy(np.frombuffer(b"".join(texts), dtype=np.uint8).copy()).pin_memory().numpy()
+    res, codes = bv.run_json((blob, offs))
+    assert (codes == 0).all() and (res == 1).all()
+    t = time.perf_counter()
+    for _ in range(steps):
+        res, codes = bv.run_json((blob, offs))
+    dt = (time.perf_counter() - t) / steps
+    assert (res == 1).all()
+    return {"value": round(B / dt, 1), "unit": "proofs/s", "ms_per_step": round(dt * 1e3, 3),
+            "note": f"{B} JSON proofs ({blob.nbytes / 1e6:.0f} MB, pinned) per step: H2D + device packing + verify, one batch at a time"}
+
+
 def h2d_rate(bv, tiled, B, expect, steps=3):
     """PCIe-inclusive: packed proofs in pinned host memory, H2D copy inside the timed run."""
     import torch
@@ -333,6 +353,7 @@ def main():
         if world == 1 and not args.quick:
             out["ingest"] = ingest_rate(vk, proofs, threads)
             out["h2d_end_to_end"] = h2d_rate(bvs[0], tiled, B, expect)
+            out["json_end_to_end"] = json_rate(bvs[0], proofs, B)
         if world == 1 and not args.no_cpu_baseline and not args.quick:
             out["cpu_baseline"] = cpu_baseline(gc, proofs, threads)
         print(json.dumps(out), flush=True)

@@ -122,6 +122,18 @@ void p2v_verifier_free(p2v_verifier* v);
 int  p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n,
                       int8_t* results, uint64_t* trace, void* stream, uint32_t flags);
 
+/* Verify n proofs given as ProofWithPublicInputs JSON texts (Types.hs:245-279) in host memory:
+ * proof i is blob[offsets[i] .. offsets[i+1]) (n + 1 offsets; pinned memory makes the copy
+ * fastest).  The texts are copied to the device and packed there against a template taken
+ * from the batch's first decodable proof (json_pack.hip); a proof that does not fit the
+ * template is packed by the host reader instead, so the packed words and the decode codes
+ * (codes[i]: P2V_OK / P2V_E_PARSE / P2V_E_SHAPE) are those of p2v_pack_proof_json.  Proofs
+ * that do not decode get results[i] = P2V_ERR_PARSE / P2V_ERR_SHAPE.  Host results only.
+ * n_device (optional, may be NULL) receives how many proofs the device packer took.
+ * Replaces: decode + verifyProof per proof (Types.hs:245-254, Plonk/Verifier.hs:56-65). */
+int  p2v_verifier_run_json(p2v_verifier* v, const char* blob, const uint64_t* offsets, size_t n,
+                           int8_t* results, int32_t* codes, size_t* n_device, void* stream);
+
 /* One-shot convenience: create a verifier on `device`, verify, free. */
 int  p2v_verify_batch(const p2v_circuit* c, const uint64_t* proofs, size_t n,
                       int8_t* results, int device);

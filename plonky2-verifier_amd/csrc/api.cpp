@@ -22,6 +22,7 @@ extern "C" __global__ void k_vanish(DevCircuit);
 extern "C" __global__ void k_lut(DevCircuit);
 extern "C" __global__ void k_vanish_final(DevCircuit);
 extern "C" __global__ void k_status(DevCircuit, int8_t*, uint64_t*, int64_t);
+extern "C" __global__ void k_json_pack(const uint8_t*, const uint64_t*, int, const uint8_t*, int64_t, const int32_t*, int64_t, uint64_t*, int64_t, int8_t*);
 
 using namespace p2v;
 
@@ -71,6 +72,12 @@ struct p2v_verifier {
   int transcript_mode = 0;          // 0 auto, 1 row, 2 quad (env P2V_TRANSCRIPT)
   int quad_min_batch = 2048;        // auto: quad form from this batch size on
   bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
+  // JSON ingest on the device (p2v_verifier_run_json): the current template and its device
+  // form, and buffers grown on demand
+  ProofTemplate tmpl;
+  bool have_tmpl = false;
+  int64_t skel_len = 0, ntok = 0;
+  DevBuf j_blob, j_offs, j_skel, j_tok, j_ok;
 };
 
 extern "C" {
@@ -179,7 +186,7 @@ void p2v_verifier_free(p2v_verifier* v) {
   if (!v) return;
   (void)hipSetDevice(v->device);
   for (DevBuf* b : {&v->in, &v->soa, &v->chal, &v->leafdig, &v->mk, &v->fbits, &v->qvals, &v->van, &v->vparts, &v->lutre, &v->res, &v->trace, &v->t_cs, &v->t_kis,
-                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit, &v->t_rin, &v->t_rout, &v->t_roff, &v->t_rch, &v->t_pbase, &v->lutpart})
+                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit, &v->t_rin, &v->t_rout, &v->t_roff, &v->t_rch, &v->t_pbase, &v->lutpart, &v->j_blob, &v->j_offs, &v->j_skel, &v->j_tok, &v->j_ok})
     b->free_();
   if (v->timed) for (auto& e : v->ev) (void)hipEventDestroy(e);
   if (v->dep_p1) (void)hipEventDestroy(v->dep_p1);
@@ -470,6 +477,76 @@ int p2v_verify_batch_devices(const p2v_circuit* c, const uint64_t* proofs, size_
   for (auto& t : pool) t.join();
   for (int s = 0; s < shards; s++)
     if (rcs[s] != P2V_OK) return fail(rcs[s], "shard " + std::to_string(s) + " (device " + std::to_string(devices[s]) + "): " + msgs[s]);
+  return P2V_OK;
+}
+
+int p2v_verifier_run_json(p2v_verifier* v, const char* blob, const uint64_t* offsets, size_t n,
+                          int8_t* results, int32_t* codes, size_t* n_device, void* stream_) {
+  if (n_device) *n_device = 0;
+  if (!v || (n && (!blob || !offsets || !results || !codes))) return fail(P2V_E_ARG, "null argument");
+  if (n > v->max_batch) return fail(P2V_E_ARG, "batch larger than max_batch");
+  if (n == 0) return P2V_OK;
+  HCK(hipSetDevice(v->device));
+  hipStream_t st = (hipStream_t)stream_;
+  const Circuit& C = v->circ->c;
+  const int64_t W = C.L.words;
+  auto text = [&](size_t i) { return blob + offsets[i]; };
+  auto tlen = [&](size_t i) { return (size_t)(offsets[i + 1] - offsets[i]); };
+  std::vector<uint64_t> row((size_t)W);
+  // template: keep the current one while it packs the batch's first proof, else rebuild it
+  // from the first proof the full reader accepts
+  bool fresh = false;
+  if (!(v->have_tmpl && v->tmpl.pack(text(0), tlen(0), row.data()))) {
+    v->have_tmpl = false;
+    for (size_t i = 0; i < n && !v->have_tmpl && i < 64; i++) {
+      try { v->have_tmpl = v->tmpl.build(C, text(i), tlen(i), row.data()); } catch (...) { v->have_tmpl = false; }
+    }
+    fresh = v->have_tmpl;
+  }
+  std::vector<uint8_t> skel; std::vector<int32_t> tok;
+  const bool dev_ok = v->have_tmpl && (!fresh || v->tmpl.device_form(skel, tok));
+  if (fresh && dev_ok) {
+    auto put = [&](DevBuf& b, const void* h, size_t bytes) -> hipError_t {
+      if (b.bytes < bytes + 64) { b.free_(); hipError_t e = b.alloc(bytes + 64); if (e != hipSuccess) return e; }   // + vector-load slack
+      return hipMemcpy(b.p, h, bytes, hipMemcpyHostToDevice);
+    };
+    HCK(put(v->j_skel, skel.data(), skel.size()));
+    HCK(put(v->j_tok, tok.data(), tok.size() * sizeof(int32_t)));
+    v->skel_len = (int64_t)skel.size(); v->ntok = (int64_t)tok.size();
+  }
+  std::vector<int8_t> okf(n, 0);
+  if (dev_ok && v->ntok > 0) {
+    const uint64_t base = offsets[0], bytes = offsets[n] - base;
+    if (v->j_blob.bytes < bytes + 64) { v->j_blob.free_(); HCK(v->j_blob.alloc(bytes + 64)); }   // + vector-load slack
+    if (v->j_offs.bytes < (n + 1) * 8) { v->j_offs.free_(); HCK(v->j_offs.alloc((n + 1) * 8)); }
+    if (v->j_ok.bytes < n) { v->j_ok.free_(); HCK(v->j_ok.alloc(n)); }
+    std::vector<uint64_t> rel(n + 1);
+    for (size_t i = 0; i <= n; i++) rel[i] = offsets[i] - base;
+    HCK(hipMemcpyAsync(v->j_blob.p, blob + base, bytes, hipMemcpyHostToDevice, st));
+    HCK(hipMemcpyAsync(v->j_offs.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+    k_json_pack<<<(unsigned)n, 256, 0, st>>>((const uint8_t*)v->j_blob.p, (const uint64_t*)v->j_offs.p, (int)n, (const uint8_t*)v->j_skel.p,
+                                             v->skel_len, (const int32_t*)v->j_tok.p, v->ntok, (uint64_t*)v->in.p, W, (int8_t*)v->j_ok.p);
+    HCK(hipGetLastError());
+    HCK(hipMemcpyAsync(okf.data(), v->j_ok.p, n, hipMemcpyDeviceToHost, st));
+    HCK(hipStreamSynchronize(st));
+  }
+  if (n_device) for (size_t i = 0; i < n; i++) *n_device += okf[i] ? 1 : 0;
+  // the rest (other formatting, exotic numbers, errors): the host reader, as p2v_pack_proof_json
+  for (size_t i = 0; i < n; i++) {
+    codes[i] = P2V_OK;
+    if (okf[i]) continue;
+    try {
+      JVal pj = parse_json(text(i), tlen(i));
+      pack_proof(C, pj, row.data());
+      HCK(hipMemcpyAsync((uint64_t*)v->in.p + i * W, row.data(), (size_t)W * 8, hipMemcpyHostToDevice, st));
+      HCK(hipStreamSynchronize(st));   // row is reused
+    } catch (const ShapeError&) { codes[i] = P2V_E_SHAPE; }
+    catch (...) { codes[i] = P2V_E_PARSE; }
+  }
+  int rc = p2v_verifier_run(v, (const uint64_t*)v->in.p, n, results, nullptr, stream_, P2V_FLAG_INPUT_DEVICE);
+  if (rc != P2V_OK) return rc;
+  for (size_t i = 0; i < n; i++)
+    if (codes[i] != P2V_OK) results[i] = codes[i] == P2V_E_SHAPE ? P2V_ERR_SHAPE : P2V_ERR_PARSE;
   return P2V_OK;
 }
 

@@ -454,6 +454,23 @@ inline bool same(const char* a, const char* b, size_t n) {
 }
 }  // namespace
 
+bool ProofTemplate::device_form(std::vector<uint8_t>& skel, std::vector<int32_t>& tok_dst) const {
+  auto numc = [](char c) { return (c >= '0' && c <= '9') || c == '-'; };
+  skel.clear(); tok_dst.clear();
+  size_t k = 0, i = 0;
+  const size_t n = text.size();
+  while (i < n) {
+    if (!numc(text[i])) { skel.push_back((uint8_t)text[i]); i++; continue; }
+    size_t j = i;
+    while (j < n && numc(text[j])) j++;
+    if (k >= spans.size() || spans[k].first != i || spans[k].second != j) return false;
+    tok_dst.push_back((int32_t)dst_of[k]);
+    k++;
+    i = j;
+  }
+  return k == spans.size();
+}
+
 bool ProofTemplate::pack(const char* s, size_t n, uint64_t* dst) const {
   const char* t = text.data();
   size_t ps = 0, pt = 0;

@@ -78,6 +78,11 @@ struct ProofTemplate {
   std::vector<int64_t> dst_of;                    // number ordinal -> packed word (-1: unused)
   bool build(const Circuit& c, const char* s, size_t n, uint64_t* dst);   // throws like pack_proof
   bool pack(const char* s, size_t n, uint64_t* dst) const;
+  // the device form of the template (json_pack.hip): the skeleton (every byte outside the
+  // number tokens, concatenated) and the packed word of each token.  False when a byte-level
+  // scan for runs of [0-9-] would not find exactly the template's number tokens (e.g. digits
+  // inside a key): the device path is then unusable for this template.
+  bool device_form(std::vector<uint8_t>& skel, std::vector<int32_t>& tok_dst) const;
 };
 GateDesc parse_gate_string(const std::string& s);              // Gate/Parser.hs:107-130
 

@@ -2,4 +2,5 @@
 // from the same TU that defines them; no relocatable device code needed).
 #include "kernels.hip"
 #include "vanish.hip"
+#include "json_pack.hip"
 #include "api.cpp"

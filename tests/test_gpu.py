@@ -6,6 +6,7 @@ values, per-query combineInitial / folded / final-polynomial values) must equal 
 oracle's word for word.  Integer arithmetic: no tolerance anywhere."""
 import gzip
 import json
+import re
 import os
 
 import numpy as np
@@ -232,3 +233,36 @@ def test_gpu_constraint_programs_vs_oracle_unit_filters(p2v, nb, lk):
         _, otr = O.verify_json(gc.common, gc.vkey, proof, trace=True, unit_filters=True)
         assert np.array_equal(tr[i], otr), (i, np.nonzero(tr[i] != otr)[0][:10])
         assert not np.array_equal(tr[i][o_c:o_c + 2 * r], tr0[i][o_c:o_c + 2 * r])   # the mode is live
+
+
+def test_gpu_json_ingest_matches_host_packer(p2v):
+    """p2v_verifier_run_json: JSON texts packed on the device against a template.  Proofs in
+    the template's format take the device path; other formatting, exotic numbers and
+    malformed texts must fall back to the host reader: statuses and decode codes must equal
+    host packing (p2v_pack_proofs_json) + p2v_verifier_run on every proof."""
+    from support import P
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    base = [gc.proof(1 + i % 2, 50 + i) for i in range(6)] + [gc.proof(1, 4, flags=1), gc.proof(1, 5, flags=2)]
+    pw = json.loads(base[3])["proof"]["opening_proof"]["pow_witness"]
+    key = b'"pow_witness":%d' % pw
+    edits = [b"-%d" % pw, b"%d" % (pw + 3 * P), b"%d" % (pw + P), b"0000000000000000000000%d" % pw, b"-0", b"1e5", b"12.0", b"-", b"1-2"]
+    variants = [base[3].replace(key, b'"pow_witness":' + e) for e in edits]
+    variants += [json.dumps(json.loads(base[4]), indent=1).encode(), base[2][:-9], b"[]"]
+    texts = base + variants + base[:3]
+    codes_h = np.empty(len(texts), np.int32)
+    packed = vk.pack_many(texts, codes=codes_h)
+    ok = codes_h == 0
+    want = np.where(ok, 0, np.where(codes_h == -3, -5, -7)).astype(np.int8)
+    bv = p2v.BatchVerifier(vk, 0, len(texts))
+    want[ok] = bv.run(np.ascontiguousarray(packed[ok]))
+    res, codes = bv.run_json(texts)
+    assert list(codes) == list(codes_h)
+    assert list(res) == list(want)
+    # the device packer took every proof in the template's format, numbers of <= 20 digits
+    # with an optional '-' included; everything else went through the host reader
+    n_fmt = len(base) + 3 + sum(1 for e in edits if re.fullmatch(rb"-?[0-9]{1,20}", e))
+    assert bv.last_json_device == n_fmt
+    assert sorted(set(want.tolist())) == [-7, -3, 0, 1]
+    res2, _ = bv.run_json(texts[::-1])   # a second batch reuses (or rebuilds) the template
+    assert list(res2) == list(want[::-1])
