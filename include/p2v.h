@@ -134,6 +134,13 @@ int  p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n,
 int  p2v_verifier_run_json(p2v_verifier* v, const char* blob, const uint64_t* offsets, size_t n,
                            int8_t* results, int32_t* codes, size_t* n_device, void* stream);
 
+/* The packing half of p2v_verifier_run_json: the texts are packed on the device as there, and
+ * the n * proof_words packed words copied to `words` (host memory; rows of proofs that do not
+ * decode are zero).  Bit-identical to p2v_pack_proofs_json.
+ * Replaces: decode :: ProofWithPublicInputs over a batch (Types.hs:245-254). */
+int  p2v_verifier_pack_json(p2v_verifier* v, const char* blob, const uint64_t* offsets, size_t n,
+                            int32_t* codes, size_t* n_device, uint64_t* words, void* stream);
+
 /* One-shot convenience: create a verifier on `device`, verify, free. */
 int  p2v_verify_batch(const p2v_circuit* c, const uint64_t* proofs, size_t n,
                       int8_t* results, int device);

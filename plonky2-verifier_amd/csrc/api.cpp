@@ -480,10 +480,12 @@ int p2v_verify_batch_devices(const p2v_circuit* c, const uint64_t* proofs, size_
   return P2V_OK;
 }
 
-int p2v_verifier_run_json(p2v_verifier* v, const char* blob, const uint64_t* offsets, size_t n,
-                          int8_t* results, int32_t* codes, size_t* n_device, void* stream_) {
+// JSON texts -> packed rows of v->in (device packer against the template, host reader for
+// the rest); codes[i] as p2v_pack_proof_json
+static int pack_json_into(p2v_verifier* v, const char* blob, const uint64_t* offsets, size_t n,
+                          int32_t* codes, size_t* n_device, void* stream_) {
   if (n_device) *n_device = 0;
-  if (!v || (n && (!blob || !offsets || !results || !codes))) return fail(P2V_E_ARG, "null argument");
+  if (!v || (n && (!blob || !offsets || !codes))) return fail(P2V_E_ARG, "null argument");
   if (n > v->max_batch) return fail(P2V_E_ARG, "batch larger than max_batch");
   if (n == 0) return P2V_OK;
   HCK(hipSetDevice(v->device));
@@ -543,7 +545,28 @@ int p2v_verifier_run_json(p2v_verifier* v, const char* blob, const uint64_t* off
     } catch (const ShapeError&) { codes[i] = P2V_E_SHAPE; }
     catch (...) { codes[i] = P2V_E_PARSE; }
   }
-  int rc = p2v_verifier_run(v, (const uint64_t*)v->in.p, n, results, nullptr, stream_, P2V_FLAG_INPUT_DEVICE);
+  return P2V_OK;
+}
+
+int p2v_verifier_pack_json(p2v_verifier* v, const char* blob, const uint64_t* offsets, size_t n,
+                           int32_t* codes, size_t* n_device, uint64_t* words, void* stream_) {
+  int rc = pack_json_into(v, blob, offsets, n, codes, n_device, stream_);
+  if (rc != P2V_OK || n == 0 || !words) return rc;
+  hipStream_t st = (hipStream_t)stream_;
+  const size_t W = (size_t)v->circ->c.L.words;
+  HCK(hipMemcpyAsync(words, v->in.p, n * W * 8, hipMemcpyDeviceToHost, st));
+  HCK(hipStreamSynchronize(st));
+  for (size_t i = 0; i < n; i++)
+    if (codes[i] != P2V_OK) memset(words + i * W, 0, W * 8);
+  return P2V_OK;
+}
+
+int p2v_verifier_run_json(p2v_verifier* v, const char* blob, const uint64_t* offsets, size_t n,
+                          int8_t* results, int32_t* codes, size_t* n_device, void* stream_) {
+  if (n && !results) return fail(P2V_E_ARG, "null argument");
+  int rc = pack_json_into(v, blob, offsets, n, codes, n_device, stream_);
+  if (rc != P2V_OK || n == 0) return rc;
+  rc = p2v_verifier_run(v, (const uint64_t*)v->in.p, n, results, nullptr, stream_, P2V_FLAG_INPUT_DEVICE);
   if (rc != P2V_OK) return rc;
   for (size_t i = 0; i < n; i++)
     if (codes[i] != P2V_OK) results[i] = codes[i] == P2V_E_SHAPE ? P2V_ERR_SHAPE : P2V_ERR_PARSE;

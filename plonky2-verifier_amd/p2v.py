@@ -113,6 +113,7 @@ def lib() -> ctypes.CDLL:
     L.p2v_verifier_free.restype = None
     L.p2v_verifier_run.argtypes = [vp, u64p, sz, i8p, u64p, vp, ctypes.c_uint32]
     L.p2v_verifier_run_json.argtypes = [vp, vp, vp, sz, i8p, vp, vp, vp]
+    L.p2v_verifier_pack_json.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp]
     L.p2v_verify_batch.argtypes = [vp, u64p, sz, i8p, ctypes.c_int]
     L.p2v_verify_batch_devices.argtypes = [vp, u64p, sz, i8p, ctypes.POINTER(ctypes.c_int), ctypes.c_int, sz]
     L.p2v_verifier_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
@@ -253,21 +254,24 @@ class BatchVerifier:
                                       tr.ctypes.data if trace else None, None, FLAG_UNIT_FILTERS if unit_filters else 0))
         return (res, tr) if trace else res
 
+    @staticmethod
+    def _json_batch(proofs):
+        if isinstance(proofs, tuple):
+            blob, offs = proofs
+            blob = np.ascontiguousarray(blob, dtype=np.uint8) if not isinstance(blob, np.ndarray) else blob
+            return blob, np.ascontiguousarray(offs, dtype=np.uint64)
+        bs = [_bytes(p) for p in proofs]
+        offs = np.zeros(len(bs) + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum([len(b) for b in bs])
+        return np.frombuffer(b"".join(bs), dtype=np.uint8), offs
+
     def run_json(self, proofs: Union[Sequence[Union[str, bytes]], tuple], stream: int = 0):
         """JSON texts -> (int8 statuses, int32 decode codes) via p2v_verifier_run_json (texts
         copied to the device and packed there).  `proofs` is a list of texts, or a pair
         (uint8 blob array, uint64 offsets[n + 1]) e.g. in pinned memory.  How many proofs the
         device packer took (the rest went through the host reader) is left in
         `self.last_json_device`."""
-        if isinstance(proofs, tuple):
-            blob, offs = proofs
-            blob = np.ascontiguousarray(blob, dtype=np.uint8) if not isinstance(blob, np.ndarray) else blob
-            offs = np.ascontiguousarray(offs, dtype=np.uint64)
-        else:
-            bs = [_bytes(p) for p in proofs]
-            offs = np.zeros(len(bs) + 1, dtype=np.uint64)
-            offs[1:] = np.cumsum([len(b) for b in bs])
-            blob = np.frombuffer(b"".join(bs), dtype=np.uint8)
+        blob, offs = self._json_batch(proofs)
         n = offs.size - 1
         res = np.empty(n, dtype=np.int8)
         codes = np.empty(n, dtype=np.int32)
@@ -276,6 +280,19 @@ class BatchVerifier:
                                            ctypes.addressof(ndev), ctypes.c_void_p(stream)))
         self.last_json_device = ndev.value
         return res, codes
+
+    def pack_json(self, proofs: Union[Sequence[Union[str, bytes]], tuple], stream: int = 0):
+        """JSON texts -> (uint64 [n, proof_words] packed words, int32 decode codes), packed on
+        the device (p2v_verifier_pack_json); same inputs as run_json."""
+        blob, offs = self._json_batch(proofs)
+        n = offs.size - 1
+        words = np.empty((n, self.circuit.info.proof_words), dtype=np.uint64)
+        codes = np.empty(n, dtype=np.int32)
+        ndev = ctypes.c_size_t(0)
+        _check(lib().p2v_verifier_pack_json(self._h, blob.ctypes.data, offs.ctypes.data, n, codes.ctypes.data,
+                                            ctypes.addressof(ndev), words.ctypes.data, ctypes.c_void_p(stream)))
+        self.last_json_device = ndev.value
+        return words, codes
 
     def run_device(self, proofs_ptr: int, n: int, results_ptr: int, stream: int = 0, trace_ptr: int = 0,
                    sync: bool = True) -> None:

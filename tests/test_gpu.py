@@ -266,3 +266,50 @@ def test_gpu_json_ingest_matches_host_packer(p2v):
     assert sorted(set(want.tolist())) == [-7, -3, 0, 1]
     res2, _ = bv.run_json(texts[::-1])   # a second batch reuses (or rebuilds) the template
     assert list(res2) == list(want[::-1])
+    words, codes3 = bv.pack_json(texts)   # the packed words themselves, bit-exact
+    assert list(codes3) == list(codes_h)
+    assert np.array_equal(words[ok], packed[ok]) and not words[~ok].any()
+
+
+def test_gpu_json_ingest_fuzz(p2v):
+    """Seeded byte-level mutations of proof texts (replace / insert / delete a byte from a
+    JSON-significant alphabet, duplicate or cut a span, long digit runs): the device packer
+    must flag exactly what it cannot pack, so the packed words and decode codes of
+    p2v_verifier_pack_json equal the host reader's on every text."""
+    rng = np.random.default_rng(1234)
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    srcs = [gc.proof(1 + i % 2, 70 + i) for i in range(4)]
+    alpha = b'0123456789-,:[]{}" .eE+x'
+    texts = list(srcs)
+    for k in range(400):
+        t = bytearray(srcs[k % len(srcs)])
+        for _ in range(1 + k % 3):
+            op, i = int(rng.integers(6)), int(rng.integers(len(t)))
+            c = alpha[int(rng.integers(len(alpha)))]
+            if op == 0:
+                t[i] = c
+            elif op == 1:
+                t.insert(i, c)
+            elif op == 2:
+                del t[i]
+            elif op == 3:
+                j = min(len(t), i + int(rng.integers(1, 40)))
+                t[i:i] = t[i:j]
+            elif op == 4:
+                t[i:i] = b"9" * int(rng.integers(1, 25))
+            else:   # a digit in a number changed: stays in the template's format
+                ds = [m.start() for m in re.finditer(rb"[0-9]", bytes(t))]
+                t[ds[int(rng.integers(len(ds)))]] = ord("0") + int(rng.integers(10))
+        texts.append(bytes(t))
+    texts.append(srcs[0][: len(srcs[0]) // 2])
+    codes_h = np.empty(len(texts), np.int32)
+    packed = vk.pack_many(texts, codes=codes_h)
+    ok = codes_h == 0
+    bv = p2v.BatchVerifier(vk, 0, len(texts))
+    words, codes = bv.pack_json(texts)
+    assert list(codes) == list(codes_h)
+    assert np.array_equal(words[ok], packed[ok])
+    print("device-packed", bv.last_json_device, "of", int(ok.sum()), "decodable")
+    assert bv.last_json_device >= 80   # the device path carried the format-preserving edits
+    assert ok.sum() < len(texts)                     # and the host reader saw real failures
