@@ -147,8 +147,9 @@ int  p2v_verify_batch(const p2v_circuit* c, const uint64_t* proofs, size_t n,
 
 /* Single-process multi-GPU form of p2v_verify_batch: the batch (host memory,
  * proof-major) is split into ndevices contiguous near-equal shards, shard i verified on
- * devices[i] (a device may repeat) by its own host thread, stream and verifier, in chunks of
- * at most `chunk` proofs (0: 16384) copied H2D per chunk.  Proofs are independent, so there is
+ * devices[i] (a device may repeat), in chunks of at most `chunk` proofs (0: 16384) copied H2D
+ * per chunk.  Each shard has two workers (a host thread, stream and verifier each) taking
+ * alternate chunks, so one chunk's copy overlaps another's verification.  Proofs are independent, so there is
  * no cross-device traffic.  On failure returns the first failing shard's code and message.
  * Replaces: map (verifyProof vkey) over a batch (Plonk/Verifier.hs:56-65) on N GPUs. */
 int  p2v_verify_batch_devices(const p2v_circuit* c, const uint64_t* proofs, size_t n, int8_t* results,

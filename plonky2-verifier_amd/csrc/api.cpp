@@ -454,29 +454,35 @@ int p2v_verify_batch_devices(const p2v_circuit* c, const uint64_t* proofs, size_
   if (chunk == 0) chunk = 16384;
   const size_t W = (size_t)c->c.L.words;
   const int shards = (int)std::min<size_t>((size_t)ndevices, n);
-  std::vector<int> rcs(shards, P2V_OK);
-  std::vector<std::string> msgs(shards);
-  auto work = [&](int s) {
+  // two workers per shard (own host thread, stream and verifier), taking alternate chunks, so
+  // one chunk's H2D copy overlaps the other's verification on the same device
+  constexpr int kWorkers = 2;
+  std::vector<int> rcs(shards * kWorkers, P2V_OK);
+  std::vector<std::string> msgs(shards * kWorkers);
+  auto work = [&](int s, int k) {
     const size_t base = n / shards, extra = n % shards;   // p2v.shard_bounds
     const size_t a = s * base + std::min<size_t>(s, extra), b = a + base + ((size_t)s < extra ? 1 : 0);
+    if (a + k * chunk >= b) return;   // no chunk for this worker
     int rc = P2V_OK;
     p2v_verifier* v = nullptr;
     hipStream_t st = nullptr;
     if (hipSetDevice(devices[s]) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
       rc = fail(P2V_E_DEVICE, "stream creation on device " + std::to_string(devices[s]));
     if (rc == P2V_OK) rc = p2v_verifier_create(c, devices[s], std::min(chunk, b - a), &v);
-    for (size_t i = a; rc == P2V_OK && i < b; i += chunk)
+    for (size_t i = a + k * chunk; rc == P2V_OK && i < b; i += kWorkers * chunk)
       rc = p2v_verifier_run(v, proofs + i * W, std::min(chunk, b - i), results + i, nullptr, st, 0);
-    if (rc != P2V_OK) msgs[s] = g_err;   // g_err is thread-local: carry the message back
-    rcs[s] = rc;
+    if (rc != P2V_OK) msgs[s * kWorkers + k] = g_err;   // g_err is thread-local: carry the message back
+    rcs[s * kWorkers + k] = rc;
     p2v_verifier_free(v);
     if (st) (void)hipStreamDestroy(st);
   };
   std::vector<std::thread> pool;
-  for (int s = 0; s < shards; s++) pool.emplace_back(work, s);
-  for (auto& t : pool) t.join();
   for (int s = 0; s < shards; s++)
-    if (rcs[s] != P2V_OK) return fail(rcs[s], "shard " + std::to_string(s) + " (device " + std::to_string(devices[s]) + "): " + msgs[s]);
+    for (int k = 0; k < kWorkers; k++) pool.emplace_back(work, s, k);
+  for (auto& t : pool) t.join();
+  for (int s = 0; s < shards * kWorkers; s++)
+    if (rcs[s] != P2V_OK)
+      return fail(rcs[s], "shard " + std::to_string(s / kWorkers) + " (device " + std::to_string(devices[s / kWorkers]) + "): " + msgs[s]);
   return P2V_OK;
 }
 
