@@ -78,6 +78,9 @@ struct p2v_verifier {
   bool have_tmpl = false;
   int64_t skel_len = 0, ntok = 0;
   DevBuf j_blob, j_offs, j_skel, j_tok, j_ok;
+  // pinned host staging for the small device->host results (statuses, JSON ok flags): a copy
+  // to pageable memory would stage through the runtime and stall the other streams' work
+  int8_t* h_res = nullptr;
 };
 
 extern "C" {
@@ -192,6 +195,7 @@ void p2v_verifier_free(p2v_verifier* v) {
   if (v->dep_p1) (void)hipEventDestroy(v->dep_p1);
   if (v->dep_side) (void)hipEventDestroy(v->dep_side);
   if (v->side) (void)hipStreamDestroy(v->side);
+  if (v->h_res) (void)hipHostFree(v->h_res);
   delete v;
 }
 
@@ -344,6 +348,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (e == hipSuccess) e = v->lutre.alloc((size_t)d.r * (d.nluts ? d.nluts : 1) * B * 8);
   if (e == hipSuccess) e = v->lutpart.alloc((size_t)d.r * (d.n_lut_pieces ? d.n_lut_pieces : 1) * B * 8);
   if (e == hipSuccess) e = v->res.alloc(B);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&v->h_res, B);
   if (e == hipSuccess) e = v->trace.alloc((size_t)C.trace_words * B * 8);
   if (e == hipSuccess) { for (auto& x : v->ev) { e = hipEventCreate(&x); if (e != hipSuccess) break; } v->timed = e == hipSuccess; }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_p1, hipEventDisableTiming);
@@ -433,11 +438,12 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
 #undef T1
   HCK(hipGetLastError());
   if (!(flags & P2V_FLAG_RESULT_DEVICE)) {
-    HCK(hipMemcpyAsync(results, dres, n, hipMemcpyDeviceToHost, st));
+    HCK(hipMemcpyAsync(v->h_res, dres, n, hipMemcpyDeviceToHost, st));
     if (trace) HCK(hipMemcpyAsync(trace, dtrace, (size_t)C.trace_words * n * 8, hipMemcpyDeviceToHost, st));
   }
   if (!(flags & P2V_FLAG_NO_SYNC) || !(flags & P2V_FLAG_RESULT_DEVICE)) {
     HCK(hipStreamSynchronize(st));
+    if (!(flags & P2V_FLAG_RESULT_DEVICE)) memcpy(results, v->h_res, n);
     if (tm) for (int k = 0; k < kNumKernels; k++) { float ms = 0; if (hipEventElapsedTime(&ms, v->ev[2 * k], v->ev[2 * k + 1]) == hipSuccess) v->last_ms[k] = ms; }
   }
   return P2V_OK;
@@ -535,8 +541,9 @@ static int pack_json_into(p2v_verifier* v, const char* blob, const uint64_t* off
     k_json_pack<<<(unsigned)n, 256, 0, st>>>((const uint8_t*)v->j_blob.p, (const uint64_t*)v->j_offs.p, (int)n, (const uint8_t*)v->j_skel.p,
                                              v->skel_len, (const int32_t*)v->j_tok.p, v->ntok, (uint64_t*)v->in.p, W, (int8_t*)v->j_ok.p);
     HCK(hipGetLastError());
-    HCK(hipMemcpyAsync(okf.data(), v->j_ok.p, n, hipMemcpyDeviceToHost, st));
+    HCK(hipMemcpyAsync(v->h_res, v->j_ok.p, n, hipMemcpyDeviceToHost, st));
     HCK(hipStreamSynchronize(st));
+    memcpy(okf.data(), v->h_res, n);
   }
   if (n_device) for (size_t i = 0; i < n; i++) *n_device += okf[i] ? 1 : 0;
   // the rest (other formatting, exotic numbers, errors): the host reader, as p2v_pack_proof_json

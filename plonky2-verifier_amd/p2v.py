@@ -243,15 +243,17 @@ class BatchVerifier:
         _check(lib().p2v_verifier_create(circuit.handle, device, max_batch, ctypes.byref(h)))
         self._h = h
 
-    def run(self, proofs: np.ndarray, trace: bool = False, unit_filters: bool = False):
+    def run(self, proofs: np.ndarray, trace: bool = False, unit_filters: bool = False, stream: int = 0):
         """proofs: uint64 [n, proof_words] host array.  Returns int8 statuses (and trace).
-        unit_filters: parity mode (P2V_FLAG_UNIT_FILTERS), statuses meaningless."""
+        unit_filters: parity mode (P2V_FLAG_UNIT_FILTERS), statuses meaningless.  stream: a
+        hipStream_t handle (0: the default stream)."""
         proofs = np.ascontiguousarray(proofs, dtype=np.uint64)
         n = proofs.shape[0]
         res = np.empty(n, dtype=np.int8)
         tr = np.empty((n, self.circuit.info.trace_words), dtype=np.uint64) if trace else None
         _check(lib().p2v_verifier_run(self._h, proofs.ctypes.data, n, res.ctypes.data,
-                                      tr.ctypes.data if trace else None, None, FLAG_UNIT_FILTERS if unit_filters else 0))
+                                      tr.ctypes.data if trace else None, ctypes.c_void_p(stream) if stream else None,
+                                      FLAG_UNIT_FILTERS if unit_filters else 0))
         return (res, tr) if trace else res
 
     @staticmethod
