@@ -53,7 +53,7 @@ def valu_roofline(kavg, ms_step, B):
     scale = B / 4096.0   # the PMC pass ran 4096-proof batches
     per = {}
     for k, n in ins.items():
-        if kavg.get(k):
+        if kavg.get(k) and B == 4096:   # per-kernel shares only at the PMC pass's own batch size
             per[k] = round(n * scale / (kavg[k] * 1e-3) / 1e9 / VALU_PEAK_G_WAVE_INSTS, 3)
     tot = sum(ins.values()) * scale
     return {"unit": "G wave-instr/s", "peak": VALU_PEAK_G_WAVE_INSTS,
@@ -362,7 +362,10 @@ def main():
     kavg = {k: float(np.mean(v)) for k, v in ktimes.items()}
     if rank == 0:
         kb = kernel_bytes_model(info, info.trace_words)
-        dom = max(kavg, key=kavg.get)
+        # dominant kernel: the longest launch on the main stream (k_vanish / k_fri / k_lut run on
+        # the side stream under k_merkle and do not set the step time)
+        main_stream = [k for k in ("k_transpose", "k_phase1", "k_merkle", "k_status") if k in kavg]
+        dom = max(main_stream, key=kavg.get)
         achieved = kb[dom] * B / (kavg[dom] * 1e-3) / 1e9
         # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
         # (profiles/pmc_traffic.json, corrected per MI355X_MICROARCH.md §HBM), as GB/s over
@@ -373,6 +376,7 @@ def main():
             try:
                 traffic_bytes = json.load(open(pmc)).get(dom)
                 if traffic_bytes:
+                    traffic_bytes = int(traffic_bytes * B / 4096)   # the PMC passes ran 4096-proof batches
                     traffic = round(traffic_bytes / (kavg[dom] * 1e-3) / 1e9, 2)
             except Exception:
                 traffic = None
