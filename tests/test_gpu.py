@@ -105,6 +105,20 @@ def test_gpu_ragged_batch_sizes(p2v, n):
     assert list(res) == [1 if i % 5 else 0 for i in range(n)]
 
 
+def test_gpu_empty_and_oversized_batches(p2v):
+    """n = 0 is a no-op that returns OK (no launch); n > max_batch is an argument error and
+    writes nothing."""
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    bv = p2v.BatchVerifier(vk, 0, 64)
+    empty = np.zeros((0, vk.info.proof_words), dtype=np.uint64)
+    assert bv.run(empty).shape == (0,)
+    good = vk.pack(gc.proof(1, 1))
+    with pytest.raises(p2v.P2VError):
+        bv.run(np.stack([good] * 65))
+    assert list(bv.run(np.stack([good] * 64))) == [1] * 64
+
+
 def test_gpu_full_size_properties(p2v):
     """4096 std-config proofs (BASELINE configs[1] size): every valid proof accepts, a
     single corrupted lane flips only itself (lane isolation), and re-running the same

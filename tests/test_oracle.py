@@ -158,3 +158,19 @@ def test_golden_fixtures_oracle():
         st, tr = O.verify_json(common, vkey, rd(case["name"] + "_proof.json.gz"), trace=True)
         assert st == case["status"], case["name"]
         assert [int(x) for x in tr] == [int(x) for x in case["trace"]], case["name"]
+
+
+def test_coset_gate_matches_reference_example():
+    """Gate/Parser.hs:150 quotes a CosetInterpolationGate string from a real Plonky2 circuit:
+    `subgroup_bits: 4, degree: 6, barycentric_weights: [17293822565076172801, ...`.  The
+    generator derives degree and weights itself (CosetInterp.hs:36-49: w_i = 1/prod_{j!=i}
+    (x_i - x_j) over the size-16 subgroup, so w_0 = 1/16); the reference's example pins both,
+    and with them the field inverse and the 2-adic subgroup generator."""
+    gc = gen_circuit(6, 4, 0)
+    gates = [g for g in json.loads(gc.common)["gates"] if g.startswith("CosetInterpolationGate")]
+    assert gates
+    assert gates[0].startswith("CosetInterpolationGate { subgroup_bits: 4, degree: 6, "
+                               "barycentric_weights: [17293822565076172801, ")
+    assert oracle().L.or_gate_kind(gates[0].encode()) == oracle().L.or_gate_kind(
+        b"CosetInterpolationGate { subgroup_bits: 4, degree: 6, barycentric_weights: [17293822565076172801], "
+        b"_phantom: PhantomData<plonky2_field::goldilocks_field::GoldilocksField> }<D=2>")
