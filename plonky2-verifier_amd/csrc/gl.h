@@ -68,6 +68,10 @@ GL_HD uint64_t reduce96_nc(uint64_t hi, uint64_t lo) {
   return r;
 }
 
+#ifndef P2V_MUL_MERGED
+#define P2V_MUL_MERGED 1   // one net wrap fix-up in mul_nc_dev (14 VALU instead of 16)
+#endif
+
 #if defined(__HIP_DEVICE_COMPILE__)
 // gfx950 carry-chain primitives.  The compiler does not use the carry-out of
 // v_mad_u64_u32 / v_add_co_u32 and re-derives every carry with a 64-bit compare; these
@@ -85,6 +89,8 @@ __device__ __forceinline__ uint32_t sub_co(uint32_t a, uint32_t b, uint64_t& co)
 __device__ __forceinline__ uint32_t subb_co(uint32_t a, uint32_t b, uint64_t ci, uint64_t& co) { uint32_t d; asm("v_subb_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(a), "v"(b), "s"(ci)); return d; }
 __device__ __forceinline__ uint32_t subb0_co(uint32_t a, uint64_t ci, uint64_t& co) { uint32_t d; asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(d), "=s"(co) : "v"(a), "s"(ci)); return d; }
 __device__ __forceinline__ uint32_t mask_m1(uint64_t m) { uint32_t d; asm("v_cndmask_b32_e64 %0, 0, -1, %1" : "=v"(d) : "s"(m)); return d; }
+__device__ __forceinline__ uint32_t sel(uint32_t a, uint32_t b, uint64_t m) { uint32_t d; asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(m)); return d; }
+__device__ __forceinline__ uint64_t add64(uint64_t a, uint64_t b) { uint64_t d; asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(d) : "v"(a), "v"(b)); return d; }
 __device__ __forceinline__ uint32_t mask_1(uint64_t m) { uint32_t d; asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(d) : "s"(m)); return d; }
 }  // namespace ax
 
@@ -105,6 +111,19 @@ __device__ __forceinline__ uint64_t mul_nc_dev(uint64_t a, uint64_t b) {
   const uint32_t h0 = addc_co((uint32_t)p11, (uint32_t)(m >> 32), c1, c2);
   const uint32_t h1 = addc0((uint32_t)(p11 >> 32), c2);                 // + cm: below
   const uint64_t lo = ((uint64_t)lo1 << 32) | (uint32_t)p00;
+#if P2V_MUL_MERGED
+  // lo + h0 (2^32 - 1) - (h1 + cm) = u + (c - b) 2^64 with the carry c of the MAD and the
+  // borrow b of the subtraction; one fix-up for the net wrap: +2^64 == + (2^32 - 1), and
+  // -2^64 == + p (mod 2^64 arithmetic), both without a second wrap.
+  (void)c4; (void)bw2; (void)bw3; (void)bw4;
+  const uint64_t t = madm1_co(h0, lo, ct);
+  const uint32_t ul = subb_co((uint32_t)t, h1, cm, bw1);
+  const uint32_t uh = subb0_co((uint32_t)(t >> 32), bw1, bw2);
+  const uint64_t pos = ct & ~bw2, neg = bw2 & ~ct;
+  const uint32_t kl = sel(sel(0u, 1u, neg), 0xFFFFFFFFu, pos);
+  const uint32_t kh = mask_m1(neg);
+  return add64(((uint64_t)uh << 32) | ul, ((uint64_t)kh << 32) | kl);
+#else
   const uint64_t t = madm1_co(h0, lo, ct);                              // lo + h0 (2^32 - 1)
   const uint32_t tl = add_co((uint32_t)t, mask_m1(ct), c4);             // wrapped: + 2^32 - 1
   const uint32_t th = addc0((uint32_t)(t >> 32), c4);
@@ -113,6 +132,7 @@ __device__ __forceinline__ uint64_t mul_nc_dev(uint64_t a, uint64_t b) {
   const uint32_t rl2 = sub_co(rl, mask_m1(bw2), bw3);                   // wrapped: - (2^32 - 1)
   const uint32_t rh2 = subb0_co(rh, bw3, bw4);
   return ((uint64_t)rh2 << 32) | rl2;
+#endif
 }
 #endif
 
