@@ -166,15 +166,15 @@ __device__ __forceinline__ uint64_t madk_s(uint32_t a, uint64_t acc) {   // acc 
   asm("v_mad_u64_u32 %0, s[94:95], %1, %2, %3" : "=v"(d) : "v"(a), "n"(C), "s"(acc) : "s94", "s95");
   return d;
 }
-// al + 2^32 ah (al, ah < 2^43) -> [0, 2^64), congruent mod p: t = al + ah_hi (2^32 - 1), then
-// + ah_lo 2^32 on the high word; a carry out (2^64 == 2^32 - 1) adds 2^32 - 1 back.  5 VALU.
+// al + 2^32 ah (al, ah < 2^44) -> [0, 2^64), congruent mod p: t = al + ah_hi (2^32 - 1), then
+// + ah_lo 2^32 on the high word; a carry out (2^64 == 2^32 - 1) adds (2^32 - 1) * carry back
+// with one more MAD (the wrapped sum is < 2^45, so that cannot carry).  4 VALU.
 __device__ __forceinline__ uint64_t reduce_rows(uint64_t al, uint64_t ah) {
   using namespace gl::ax;
   uint64_t c1, c2;
-  const uint64_t t = madm1_co((uint32_t)(ah >> 32), al, c1);   // < 2^44: no carry
+  const uint64_t t = madm1_co((uint32_t)(ah >> 32), al, c1);   // < 2^45: no carry
   const uint32_t rh = add_co((uint32_t)(t >> 32), (uint32_t)ah, c1);
-  const uint32_t rl = add_co((uint32_t)t, mask_m1(c1), c2);
-  return ((uint64_t)addc0(rh, c2) << 32) | rl;
+  return madm1_co(mask_1(c1), ((uint64_t)rh << 32) | (uint32_t)t, c2);
 }
 template <int I, int J>
 __device__ __forceinline__ void mds_acc(const uint64_t* s, uint64_t& al, uint64_t& ah) {
