@@ -155,6 +155,16 @@ int  p2v_verify_batch(const p2v_circuit* c, const uint64_t* proofs, size_t n,
 int  p2v_verify_batch_devices(const p2v_circuit* c, const uint64_t* proofs, size_t n, int8_t* results,
                               const int* devices, int ndevices, size_t chunk);
 
+/* Self-test of the device primitives every verifier kernel is built from, on `device`
+ * (host buffers; n items):
+ *   op 0: out[i] = a[i] * b[i] mod p, canonical            (Algebra/Goldilocks.hs:126-133)
+ *   op 1: out[12i..] = Poseidon permutation of a[12i..]     (Hash/Poseidon.hs:42-46)
+ *   op 2: out[12i..12i+4) = compress form: words 8..11 of a[12i..] taken as 0, words 0..3 of
+ *         the permutation returned, the rest 0               (Hash/Merkle.hs:21-24)
+ * Inputs may be any u64 (values >= p are congruent, as the reference reads them).
+ * Test hook for the parity suite (edge values the synthetic proofs never produce). */
+int  p2v_selftest(int device, int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n);
+
 /* Per-launch timing of the last run (milliseconds, from HIP events on the run's stream):
  * out[k] for kernel k in the order named by p2v_kernel_names(). Returns count. */
 int  p2v_verifier_last_timings(const p2v_verifier* v, float* out, int max);

@@ -68,10 +68,6 @@ GL_HD uint64_t reduce96_nc(uint64_t hi, uint64_t lo) {
   return r;
 }
 
-#ifndef P2V_MUL_MERGED
-#define P2V_MUL_MERGED 1   // one net wrap fix-up in mul_nc_dev (14 VALU instead of 16)
-#endif
-
 #if defined(__HIP_DEVICE_COMPILE__)
 // gfx950 carry-chain primitives.  The compiler does not use the carry-out of
 // v_mad_u64_u32 / v_add_co_u32 and re-derives every carry with a 64-bit compare; these
@@ -95,11 +91,16 @@ __device__ __forceinline__ uint32_t mask_1(uint64_t m) { uint32_t d; asm("v_cndm
 }  // namespace ax
 
 // a * b (mod p) for any a, b < 2^64, result in [0, 2^64) (not necessarily canonical).
-// 16 VALU: 4 partial products; the 128-bit product lo + h0 2^64 + h1 2^96 through the
-// carry chain, where the carry cm of the middle sum a0 b1 + a1 b0 (weight 2^96) is not
-// added into h1 but enters the subtraction of h1 as its borrow-in; then
-// lo + h0 (2^32 - 1) - h1 (2^64 == 2^32 - 1, 2^96 == -1 mod p) with one fix-up per wrap.
-__device__ __forceinline__ uint64_t mul_nc_dev(uint64_t a, uint64_t b) {
+// 4 partial products; the 128-bit product lo + h0 2^64 + h1 2^96 through the carry chain,
+// where the carry cm of the middle sum a0 b1 + a1 b0 (weight 2^96) is not added into h1 but
+// enters the subtraction of h1 as its borrow-in; then lo + h0 (2^32 - 1) - h1
+// (2^64 == 2^32 - 1, 2^96 == -1 mod p) and the wrap fix-ups.  V selects the fix-up form:
+//   V = 1: one fix-up for the net wrap (14 VALU), branch-free: the general multiply;
+//   V = 2: the common +2^64 wrap by one MAD, the rare -2^64 wrap in a wave-uniform branch
+//          (12 VALU when not taken): the Poseidon S-box (p2::mul_nc);
+//   V = 0: one fix-up per wrap (16 VALU), the first form, kept for measurement.
+template <int V = 1>
+__device__ __forceinline__ uint64_t mul_nc_dev_v(uint64_t a, uint64_t b) {
   using namespace ax;
   const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
   uint64_t cm, c1, c2, ct, c4, bw1, bw2, bw3, bw4;
@@ -111,7 +112,18 @@ __device__ __forceinline__ uint64_t mul_nc_dev(uint64_t a, uint64_t b) {
   const uint32_t h0 = addc_co((uint32_t)p11, (uint32_t)(m >> 32), c1, c2);
   const uint32_t h1 = addc0((uint32_t)(p11 >> 32), c2);                 // + cm: below
   const uint64_t lo = ((uint64_t)lo1 << 32) | (uint32_t)p00;
-#if P2V_MUL_MERGED
+  if constexpr (V == 2) {
+  // as below, but the -2^64 case (only when the product has bits 64..95 zero and bits 0..63
+  // below 2^32, e.g. powers of two) is a wave-uniform branch that is almost never taken
+  (void)c4; (void)bw3; (void)bw4;
+  const uint64_t t = madm1_co(h0, lo, ct);
+  const uint32_t ul = subb_co((uint32_t)t, h1, cm, bw1);
+  const uint32_t uh = subb0_co((uint32_t)(t >> 32), bw1, bw2);
+  const uint64_t pos = ct & ~bw2, neg = bw2 & ~ct;
+  uint64_t r = madm1_co(mask_1(pos), ((uint64_t)uh << 32) | ul, c4);
+  if (__builtin_expect(neg != 0, 0)) r = add64(r, ((uint64_t)mask_m1(neg) << 32) | sel(0u, 1u, neg));
+  return r;
+  } else if constexpr (V == 1) {
   // lo + h0 (2^32 - 1) - (h1 + cm) = u + (c - b) 2^64 with the carry c of the MAD and the
   // borrow b of the subtraction; one fix-up for the net wrap: +2^64 == + (2^32 - 1), and
   // -2^64 == + p (mod 2^64 arithmetic), both without a second wrap.
@@ -123,7 +135,7 @@ __device__ __forceinline__ uint64_t mul_nc_dev(uint64_t a, uint64_t b) {
   const uint32_t kl = sel(sel(0u, 1u, neg), 0xFFFFFFFFu, pos);
   const uint32_t kh = mask_m1(neg);
   return add64(((uint64_t)uh << 32) | ul, ((uint64_t)kh << 32) | kl);
-#else
+  } else {
   const uint64_t t = madm1_co(h0, lo, ct);                              // lo + h0 (2^32 - 1)
   const uint32_t tl = add_co((uint32_t)t, mask_m1(ct), c4);             // wrapped: + 2^32 - 1
   const uint32_t th = addc0((uint32_t)(t >> 32), c4);
@@ -132,8 +144,10 @@ __device__ __forceinline__ uint64_t mul_nc_dev(uint64_t a, uint64_t b) {
   const uint32_t rl2 = sub_co(rl, mask_m1(bw2), bw3);                   // wrapped: - (2^32 - 1)
   const uint32_t rh2 = subb0_co(rh, bw3, bw4);
   return ((uint64_t)rh2 << 32) | rl2;
-#endif
+  }
 }
+// the general-purpose multiply (FRI, vanishing, gates): the branch-free one-fix-up form
+__device__ __forceinline__ uint64_t mul_nc_dev(uint64_t a, uint64_t b) { return mul_nc_dev_v<1>(a, b); }
 #endif
 
 GL_HD void mul128(uint64_t a, uint64_t b, uint64_t& hi, uint64_t& lo) {

@@ -493,3 +493,24 @@ extern "C" __global__ void __launch_bounds__(256) k_status(DevCircuit c, int8_t*
     (void)S;
   }
 }
+
+// Self-test of the device field and hash primitives the verifier kernels are built from
+// (p2v_selftest): op 0 gl::mul (canonical a b mod p, Goldilocks.hs:126-133), op 1 the
+// Poseidon permutation (permute_dev, Hash/Poseidon.hs:42-46; a = n states of 12 words),
+// op 2 the 2-to-1 compression form (permute_dev(s, zh, gm = words 0..3), Hash/Merkle.hs:21-24;
+// a = n states whose words 8..11 are ignored and taken as 0).  One lane per item.
+extern "C" __global__ void __launch_bounds__(256) k_selftest(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (op == 0) {
+    out[i] = gl::mul(a[i], b[i]);
+  } else {
+    uint64_t s[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) s[k] = op == 2 && k >= 8 ? 0 : a[12 * i + k];
+    if (op == 1) p2::permute_dev(s);
+    else p2::permute_dev(s, true, 1);
+#pragma unroll
+    for (int k = 0; k < 12; k++) out[12 * i + k] = op == 2 && k >= 4 ? 0 : s[k];
+  }
+}

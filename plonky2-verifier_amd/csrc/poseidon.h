@@ -14,6 +14,10 @@
 #define P2V_POSEIDON_ASMBLK 0   // measured: no faster in the verifier kernels (VGPR pressure), see DESIGN.md §5.1
 #endif
 
+#ifndef P2V_SBOX_MUL
+#define P2V_SBOX_MUL 2   // S-box multiply form (gl::mul_nc_dev_v): 2 = rare wrap as a uniform branch
+#endif
+
 namespace p2 {
 
 static constexpr uint32_t MDS_CIRC[12] = {17, 15, 41, 16, 2, 28, 13, 13, 39, 18, 34, 20};
@@ -43,11 +47,25 @@ __host__ __device__ __forceinline__ uint64_t add_nc(uint64_t a, uint64_t b) {   
 }
 __host__ __device__ __forceinline__ uint64_t mul_nc(uint64_t a, uint64_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  return gl::mul_nc_dev(a, b);
+  return gl::mul_nc_dev_v<P2V_SBOX_MUL>(a, b);
 #else
   uint64_t hi, lo;
   gl::mul128(a, b, hi, lo);
   return gl::reduce128_nc(hi, lo);
+#endif
+}
+// x^7, latency form for the transcript chains (qposeidon.h, rposeidon.h): the branch-free
+// multiply, whose straight-line code the scheduler can interleave
+__host__ __device__ __forceinline__ uint64_t sbox_lat(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint64_t x2 = gl::mul_nc_dev(x, x), x3 = gl::mul_nc_dev(x, x2), x4 = gl::mul_nc_dev(x2, x2);
+  return gl::mul_nc_dev(x3, x4);
+#else
+  uint64_t hi, lo, x2, x3, x4;
+  gl::mul128(x, x, hi, lo); x2 = gl::reduce128_nc(hi, lo);
+  gl::mul128(x, x2, hi, lo); x3 = gl::reduce128_nc(hi, lo);
+  gl::mul128(x2, x2, hi, lo); x4 = gl::reduce128_nc(hi, lo);
+  gl::mul128(x3, x4, hi, lo); return gl::reduce128_nc(hi, lo);
 #endif
 }
 // x^7

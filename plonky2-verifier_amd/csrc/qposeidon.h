@@ -106,13 +106,13 @@ __device__ __forceinline__ void permute(uint64_t x[3], int t) {
     uint64_t al[3], ah[3];
     if (r < 4 || r >= 26) {
 #pragma unroll
-      for (int k = 0; k < 3; k++) x[k] = p2::sbox(x[k]);
+      for (int k = 0; k < 3; k++) x[k] = p2::sbox_lat(x[k]);
       mds_acc(x, t, kl, kh, al, ah);
     } else {
       const uint64_t w0 = x[0];
       x[0] = t == 0 ? 0 : w0;
       mds_acc(x, t, kl, kh, al, ah);           // independent of the S-box below
-      const uint64_t s = bcast64(p2::sbox(w0), 0);
+      const uint64_t s = bcast64(p2::sbox_lat(w0), 0);
 #pragma unroll
       for (int m = 0; m < 3; m++) {
         al[m] += (uint64_t)(uint32_t)s * col0[m];

@@ -121,10 +121,10 @@ __device__ __forceinline__ uint64_t permute(uint64_t x, const Row& R) {
     uint64_t al = nkl, ah = nkh;
     lane_rc(r + 2 <= 30 ? r + 2 : 30, R.L, nkl, nkh);   // row 30 of the split table is zero
     if (r < 4 || r >= 26) {
-      conv(R, p2::sbox(x), al, ah);
+      conv(R, p2::sbox_lat(x), al, ah);
     } else {
       conv(R, R.L == 0 ? 0 : x, al, ah);   // words 1..11: independent of the S-box chain
-      const uint64_t s = nbcast64<0>(p2::sbox(x));
+      const uint64_t s = nbcast64<0>(p2::sbox_lat(x));
       al += (uint64_t)(uint32_t)s * R.col0;
       ah += (s >> 32) * R.col0;
     }

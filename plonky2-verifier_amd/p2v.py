@@ -117,6 +117,7 @@ def lib() -> ctypes.CDLL:
     L.p2v_verify_batch.argtypes = [vp, u64p, sz, i8p, ctypes.c_int]
     L.p2v_verify_batch_devices.argtypes = [vp, u64p, sz, i8p, ctypes.POINTER(ctypes.c_int), ctypes.c_int, sz]
     L.p2v_verifier_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+    L.p2v_selftest.argtypes = [ctypes.c_int, ctypes.c_int, u64p, u64p, u64p, sz]
     L.p2v_kernel_names.restype = ctypes.c_char_p
     L.p2v_last_error_message.restype = ctypes.c_char_p
     L.p2v_version.restype = ctypes.c_char_p
@@ -325,6 +326,18 @@ def _status_to_bool(st: int) -> bool:
     if st == REJECT:
         return False
     raise VerifierError(int(st))
+
+
+def device_selftest(op: int, a: np.ndarray, b: Optional[np.ndarray] = None, device: int = 0) -> np.ndarray:
+    """p2v_selftest: the device field multiply (op 0, a * b mod p), Poseidon permutation (op 1,
+    a = [n, 12] states) or 2-to-1 compression form (op 2, words 8..11 taken as 0, words 0..3
+    returned) on `device`."""
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    n = a.shape[0]
+    out = np.zeros_like(a)
+    bb = np.ascontiguousarray(b, dtype=np.uint64) if b is not None else None
+    _check(lib().p2v_selftest(device, op, a.ctypes.data, bb.ctypes.data if bb is not None else None, out.ctypes.data, n))
+    return out
 
 
 def verify_proof(vkey: VerifierCircuitData, proof: Union[ProofWithPublicInputs, str, bytes], device: int = 0) -> bool:

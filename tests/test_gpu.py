@@ -327,3 +327,55 @@ def test_gpu_json_ingest_fuzz(p2v):
     print("device-packed", bv.last_json_device, "of", int(ok.sum()), "decodable")
     assert bv.last_json_device >= 80   # the device path carried the format-preserving edits
     assert ok.sum() < len(texts)                     # and the host reader saw real failures
+
+
+def _edge_values():
+    P = (1 << 64) - (1 << 32) + 1
+    vals = {0, 1, 2, 3, P - 2, P - 1, P, P + 1, (1 << 64) - 1, (1 << 64) - 2, (1 << 32) - 1, 1 << 32, (1 << 32) + 1}
+    for k in range(64):
+        vals |= {1 << k, (1 << k) - 1 if k else 0, P - (1 << k) if (1 << k) < P else 0}
+    return sorted(vals)
+
+
+def test_gpu_field_mul_edge_values(p2v):
+    """The device multiply (every S-box, every F/F^2 product of the verifier kernels) against
+    exact integer arithmetic on all pairs of edge values: powers of two and their neighbours,
+    p - 2^k, values >= p.  Products such as 2^48 * 2^48 = 2^96 take the rare wrap branches of
+    the reduction (bits 64..95 zero, bits 0..63 below 2^32) that random inputs never reach."""
+    P = (1 << 64) - (1 << 32) + 1
+    ev = _edge_values()
+    rng = np.random.default_rng(7)
+    rnd = [int(x) for x in rng.integers(0, 1 << 63, size=64, dtype=np.uint64) * 2 + 1]
+    pool = ev + rnd
+    a = np.array([x for x in pool for _ in pool], dtype=np.uint64)
+    b = np.array([y for _ in pool for y in pool], dtype=np.uint64)
+    out = p2v.device_selftest(0, a, b)
+    exp = np.array([(int(x) * int(y)) % P for x, y in zip(a.tolist(), b.tolist())], dtype=np.uint64)
+    bad = np.nonzero(out != exp)[0]
+    assert len(bad) == 0, [(hex(int(a[i])), hex(int(b[i])), hex(int(out[i])), hex(int(exp[i]))) for i in bad[:5]]
+
+
+def test_gpu_poseidon_permutation_vs_oracle(p2v):
+    """The device permutation and its compression form (zero capacity words, 4 output words)
+    against the oracle on the reference KAT (Hash/Poseidon.hs:27-35), edge-value states
+    (including words >= p, read mod p as the reference does) and random states."""
+    from support import KAT_IN, KAT_OUT, P
+    O = oracle()
+    ev = _edge_values()
+    rng = np.random.default_rng(11)
+    states = [KAT_IN]
+    for k in range(0, len(ev), 12):
+        chunk = ev[k:k + 12]
+        states.append((chunk + ev[:12])[:12])
+    for v in ev[::7]:
+        states.append([v] * 12)
+    states += [[int(x) for x in row] for row in rng.integers(0, 1 << 64, size=(256, 12), dtype=np.uint64)]
+    a = np.array(states, dtype=np.uint64)
+    full = p2v.device_selftest(1, a)
+    comp = p2v.device_selftest(2, a)
+    assert [int(x) for x in full[0]] == KAT_OUT
+    for i, st in enumerate(states):
+        exp = O.permute([int(x) % P for x in st])
+        assert [int(x) for x in full[i]] == exp, i
+        expc = O.permute([int(x) % P for x in st[:8]] + [0] * 4)
+        assert [int(x) for x in comp[i][:4]] == expc[:4], i
