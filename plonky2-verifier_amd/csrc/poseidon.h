@@ -14,6 +14,9 @@
 #define P2V_POSEIDON_ASMBLK 0   // measured: no faster in the verifier kernels (VGPR pressure), see DESIGN.md §5.1
 #endif
 
+#ifndef P2V_MDS_BRANCH
+#define P2V_MDS_BRANCH 1   // MDS row reduction: the rare carry fix-up in a uniform branch
+#endif
 #ifndef P2V_SBOX_MUL
 #define P2V_SBOX_MUL 2   // S-box multiply form (gl::mul_nc_dev_v): 2 = rare wrap as a uniform branch
 #endif
@@ -192,7 +195,15 @@ __device__ __forceinline__ uint64_t reduce_rows(uint64_t al, uint64_t ah) {
   uint64_t c1, c2;
   const uint64_t t = madm1_co((uint32_t)(ah >> 32), al, c1);   // < 2^45: no carry
   const uint32_t rh = add_co((uint32_t)(t >> 32), (uint32_t)ah, c1);
+#if P2V_MDS_BRANCH
+  // t >> 32 < 2^11, so the carry needs ah_lo > 2^32 - 2^11: ~2^-21 per row for data that is
+  // not chosen to hit it.  A wave-uniform branch around the fix-up: 2 VALU per row less.
+  uint64_t r = ((uint64_t)rh << 32) | (uint32_t)t;
+  if (__builtin_expect(c1 != 0, 0)) r = madm1_co(mask_1(c1), r, c2);
+  return r;
+#else
   return madm1_co(mask_1(c1), ((uint64_t)rh << 32) | (uint32_t)t, c2);
+#endif
 }
 template <int I, int J>
 __device__ __forceinline__ void mds_acc(const uint64_t* s, uint64_t& al, uint64_t& ah) {
