@@ -158,6 +158,7 @@ int  p2v_verify_batch_devices(const p2v_circuit* c, const uint64_t* proofs, size
 /* Self-test of the device primitives every verifier kernel is built from, on `device`
  * (host buffers; n items):
  *   op 0: out[i] = a[i] * b[i] mod p, canonical            (Algebra/Goldilocks.hs:126-133)
+ *   op 3: the same through the Poseidon S-box's multiply form
  *   op 1: out[12i..] = Poseidon permutation of a[12i..]     (Hash/Poseidon.hs:42-46)
  *   op 2: out[12i..12i+4) = compress form: words 8..11 of a[12i..] taken as 0, words 0..3 of
  *         the permutation returned, the rest 0               (Hash/Merkle.hs:21-24)

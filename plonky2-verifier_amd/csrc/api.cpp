@@ -588,20 +588,21 @@ int p2v_verifier_run_json(p2v_verifier* v, const char* blob, const uint64_t* off
 }
 
 int p2v_selftest(int device, int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n) {
-  if (op < 0 || op > 2 || (n && (!a || !out || (op == 0 && !b)))) return fail(P2V_E_ARG, "bad op / null argument");
+  if (op < 0 || op > 3 || (n && (!a || !out || ((op == 0 || op == 3) && !b)))) return fail(P2V_E_ARG, "bad op / null argument");
   const int ndev = p2v_device_count();
   if (ndev == 0) return fail(P2V_E_NODEVICE, "no HIP device");
   if (device < 0 || device >= ndev) return fail(P2V_E_ARG, "bad device index");
   if (n == 0) return P2V_OK;
   HCK(hipSetDevice(device));
-  const size_t w = op == 0 ? 1 : 12;
+  const bool fm = op == 0 || op == 3;
+  const size_t w = fm ? 1 : 12;
   DevBuf da, db, dout;
   auto cleanup = [&]() { da.free_(); db.free_(); dout.free_(); };
   hipError_t e = da.alloc(n * w * 8);
-  if (e == hipSuccess) e = db.alloc(op == 0 ? n * 8 : 16);
+  if (e == hipSuccess) e = db.alloc(fm ? n * 8 : 16);
   if (e == hipSuccess) e = dout.alloc(n * w * 8);
   if (e == hipSuccess) e = hipMemcpy(da.p, a, n * w * 8, hipMemcpyHostToDevice);
-  if (e == hipSuccess && op == 0) e = hipMemcpy(db.p, b, n * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess && fm) e = hipMemcpy(db.p, b, n * 8, hipMemcpyHostToDevice);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_selftest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, op, (const uint64_t*)da.p,
                        (const uint64_t*)db.p, (uint64_t*)dout.p, (int64_t)n);

@@ -495,7 +495,8 @@ extern "C" __global__ void __launch_bounds__(256) k_status(DevCircuit c, int8_t*
 }
 
 // Self-test of the device field and hash primitives the verifier kernels are built from
-// (p2v_selftest): op 0 gl::mul (canonical a b mod p, Goldilocks.hs:126-133), op 1 the
+// (p2v_selftest): op 0 gl::mul (canonical a b mod p, Goldilocks.hs:126-133), op 3 the S-box
+// multiply form (gl::mul_nc_dev_v<2>, canonicalised), op 1 the
 // Poseidon permutation (permute_dev, Hash/Poseidon.hs:42-46; a = n states of 12 words),
 // op 2 the 2-to-1 compression form (permute_dev(s, zh, gm = words 0..3), Hash/Merkle.hs:21-24;
 // a = n states whose words 8..11 are ignored and taken as 0).  One lane per item.
@@ -504,6 +505,10 @@ extern "C" __global__ void __launch_bounds__(256) k_selftest(int op, const uint6
   if (i >= n) return;
   if (op == 0) {
     out[i] = gl::mul(a[i], b[i]);
+  } else if (op == 3) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    out[i] = gl::canon(gl::mul_nc_dev_v<2>(a[i], b[i]));
+#endif
   } else {
     uint64_t s[12];
 #pragma unroll

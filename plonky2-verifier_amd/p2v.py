@@ -329,7 +329,7 @@ def _status_to_bool(st: int) -> bool:
 
 
 def device_selftest(op: int, a: np.ndarray, b: Optional[np.ndarray] = None, device: int = 0) -> np.ndarray:
-    """p2v_selftest: the device field multiply (op 0, a * b mod p), Poseidon permutation (op 1,
+    """p2v_selftest: the device field multiply (op 0, a * b mod p; op 3 the S-box's form), Poseidon permutation (op 1,
     a = [n, 12] states) or 2-to-1 compression form (op 2, words 8..11 taken as 0, words 0..3
     returned) on `device`."""
     a = np.ascontiguousarray(a, dtype=np.uint64)
