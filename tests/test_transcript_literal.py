@@ -1,4 +1,5 @@
-"""A second, independent restatement of the Fiat-Shamir transcript, checked against the oracle.
+"""A second, independent restatement of the Fiat-Shamir transcript and the FRI query rounds,
+checked against the oracle.
 
 The oracle (oracle/oracle.c) and the GPU kernels share one author's reading of the reference.
 This file is a literal Python transliteration of the transcript, written clause by clause
@@ -15,8 +16,11 @@ oracle's trace words to match:
 - PoW response
 - query indices
 
+The FRI part (below) restates combineInitial, the coset folding by the reference's own
+interpolation, and the final polynomial, and checks every query's values.
+
 test_gpu pins the GPU trace to the oracle word for word, so this check covers the device
-transcript as well. Pure Python loops, small cases only; CPU suite."""
+transcript and FRI values as well. Pure Python loops, small cases only; CPU suite."""
 import gzip
 import json
 import os
@@ -193,3 +197,209 @@ def test_literal_transcript_matches_oracle_trace(idx):
         ch["deltas"] = [0] * (4 * r)                # zero when the circuit has no lookups
     for name in got:
         assert got[name] == ch[name], (case["name"], name)
+
+
+# ---------------------------------------------------------------------------------------------
+# FRI query rounds, the same way: a literal restatement of Plonk/FRI.hs:128-327 (combineInitial,
+# prepareCoset, foldCosetWith by the reference's own O(arity^2) interpolation with
+# pow_ x (-k), foldingStep, the final polynomial), checked against the oracle's per-query
+# trace words (combineInitial value, value after the last fold, final-polynomial value).
+# The oracle folds by a 16-point iDFT instead, so the two share no folding code.
+
+def fmul(a, b):
+    return a * b % P
+
+
+def finv(a):                                       # inv x = x^(p-2): inv 0 = 0 (Goldilocks.hs:155-156)
+    return pow(a, P - 2, P)
+
+
+def fpow(x, e):                                    # pow with negative exponents (Goldilocks.hs:166-169)
+    return pow(finv(x), -e, P) if e < 0 else pow(x, e, P)
+
+
+def emul(x, y):                                    # F[X]/(X^2 - 7) (GoldilocksExt.hs:54-100)
+    return ((x[0] * y[0] + 7 * x[1] * y[1]) % P, (x[0] * y[1] + x[1] * y[0]) % P)
+
+
+def eadd(x, y):
+    return ((x[0] + y[0]) % P, (x[1] + y[1]) % P)
+
+
+def esub(x, y):
+    return ((x[0] - y[0]) % P, (x[1] - y[1]) % P)
+
+
+def escale(s, x):
+    return (s * x[0] % P, s * x[1] % P)
+
+
+def einv(x):
+    n = (x[0] * x[0] - 7 * x[1] * x[1]) % P
+    ni = finv(n)
+    return (x[0] * ni % P, (-x[1]) * ni % P)
+
+
+def epow(x, e):
+    r, b = (1, 0), x
+    while e:
+        if e & 1:
+            r = emul(r, b)
+        b = emul(b, b)
+        e >>= 1
+    return r
+
+
+def reduce_with_powers(alpha, xs):                 # sum alpha^i x_i (Goldilocks.hs:180-183)
+    acc = (0, 0)
+    for x in reversed(xs):
+        acc = eadd(x, emul(alpha, acc))
+    return acc
+
+
+def roots_of_unity():                              # Goldilocks.hs:69-71: [h^(2^(32-k)) | k <- 0..32]
+    h, out = 0x64fdd1a46201e246, []
+    x = h
+    while x != 1:
+        out.append(x)
+        x = x * x % P
+    out.append(1)
+    return list(reversed(out))
+
+
+ROOTS = roots_of_unity()
+MUL_GEN = 0xc65c18b67785d900
+
+
+def rev_bits(n, i):                                # FFT.hs:20-25
+    return int(format(i, f"0{n}b")[::-1], 2) if n else 0
+
+
+def fold_coset(beta, arity_bits, offset, xs):      # foldCosetWith, Plonk/FRI.hs:262-279
+    arity = 1 << arity_bits
+    omega = ROOTS[arity_bits]
+    ys = []
+    for k in range(arity):
+        acc = (0, 0)
+        for j in range(arity):
+            x_omega_j = fmul(offset, fpow(omega, j))
+            acc = eadd(acc, escale(fpow(x_omega_j, -k), xs[j]))
+        ys.append(acc)
+    tot, bk = (0, 0), (1, 0)
+    for y in ys:
+        tot = eadd(tot, emul(bk, y))
+        bk = emul(bk, beta)
+    return escale(finv(arity), tot)
+
+
+def fri_query_values(common, pwpi, ch):
+    """Per query: (combineInitial, value after the last folding step, final polynomial at x)."""
+    cfg = common["config"]
+    r = cfg["num_challenges"]
+    qdf = common["quotient_degree_factor"]
+    npp = -(-cfg["num_routed_wires"] // qdf)
+    logn = common["fri_params"]["degree_bits"]
+    logn_lde = logn + cfg["fri_config"]["rate_bits"]
+    proof = pwpi["proof"]
+    o = proof["openings"]
+    ext = lambda xs: [(F(a), F(b)) for a, b in xs]
+    alpha = tuple(ch["fri_alpha"])
+    zeta = tuple(ch["zeta"])
+    y0 = reduce_with_powers(alpha, ext(sum((o[k] for k in ("constants", "plonk_sigmas", "wires", "plonk_zs",
+                                                          "partial_products", "quotient_polys", "lookup_zs")), [])))
+    y1 = reduce_with_powers(alpha, ext(o["plonk_zs_next"] + o["lookup_zs_next"]))
+    strat = cfg["fri_config"]["reduction_strategy"]
+    arities = []
+    if "ConstantArityBits" in strat:               # expandReductionStrategy :341-352
+        a, fbits = strat["ConstantArityBits"]
+        lg = logn
+        while lg > fbits:
+            arities.append(a)
+            lg -= a
+    else:
+        arities = list(strat["Fixed"])
+    betas = [tuple(ch["fri_betas"][2 * i:2 * i + 2]) for i in range(len(arities))]
+    fp = proof["opening_proof"]
+    final_coeffs = ext(fp["final_poly"]["coeffs"])
+    out = []
+    for q, qr in enumerate(fp["query_round_proofs"]):
+        idx = ch["qidx"][q]
+        leaves = [[F(x) for x in lp[0]] for lp in qr["initial_trees_proof"]["evals_proofs"]]
+        consts, wires, pp_lookup, quot = leaves
+        pp, lookup = pp_lookup[:r * npp], pp_lookup[r * npp:]
+        first = consts + wires + pp + quot + lookup              # combineInitial :170-185
+        second = pp[:r] + lookup
+        g0 = reduce_with_powers(alpha, [(x, 0) for x in first])
+        g1 = reduce_with_powers(alpha, [(x, 0) for x in second])
+        omega, eta = ROOTS[logn], ROOTS[logn_lde]
+        point_x = (fmul(MUL_GEN, fpow(eta, rev_bits(logn_lde, idx))), 0)
+        loc1 = escale(omega, zeta)
+        one = emul(esub(g0, y0), einv(esub(point_x, zeta)))
+        two = emul(esub(g1, y1), einv(esub(point_x, loc1)))
+        cur = eadd(emul(epow(alpha, len(second)), one), two)
+        initial = cur
+        shift, size, qi = MUL_GEN, logn_lde, idx                 # foldingStep :291-323
+        for s, a in enumerate(arities):
+            evals = ext(qr["steps"][s]["evals"])
+            start = rev_bits(size, (qi >> a) << a)               # prepareCoset :245-256
+            offset = fmul(shift, fpow(ROOTS[size], start))
+            xs = [evals[rev_bits(a, i)] for i in range(1 << a)]  # reverseIndexBitsList
+            cur = fold_coset(betas[s], a, offset, xs)
+            shift = fpow(shift, 1 << a)
+            size, qi = size - a, qi >> a
+        x_final = fmul(shift, fpow(ROOTS[size], rev_bits(size, qi)))   # folding_query_loc :288-291
+        val, xp = (0, 0), 1
+        for c in final_coeffs:                                   # evalPolynomialAt :325-327
+            val = eadd(val, escale(xp, c))
+            xp = fmul(xp, x_final)
+        out.append((initial, cur, val))
+    return out
+
+
+@pytest.mark.parametrize("idx", range(len(_fixtures()[0])))
+def test_literal_fri_query_values_match_oracle_trace(idx):
+    cases, rd = _fixtures()
+    case = cases[idx]
+    if case["status"] < 0:
+        pytest.skip("the reference raises before the folded values exist (Merkle / evaluation error)")
+    common_b, vkey_b = rd(case["circuit"] + "_common.json.gz"), rd(case["circuit"] + "_vkey.json.gz")
+    proof_b = rd(case["name"] + "_proof.json.gz")
+    common, vkey, pwpi = json.loads(common_b), json.loads(vkey_b), json.loads(proof_b)
+    ch = proof_challenges(common, vkey, pwpi)
+    vals = fri_query_values(common, pwpi, ch)
+    _, tr = oracle().verify_json(common_b, vkey_b, proof_b, trace=True)
+    tr = [int(x) for x in tr]
+    r = common["config"]["num_challenges"]
+    S = len(pwpi["proof"]["opening_proof"]["commit_phase_merkle_caps"])
+    Q = common["config"]["fri_config"]["num_query_rounds"]
+    o_qin = 4 + 3 * r + 4 * r + 4 + 2 * S + 1 + Q + 4 * r       # include/p2v.h trace layout
+    o_qfold, o_qfin = o_qin + 2 * Q, o_qin + 4 * Q
+    for q, (ini, fold, fin) in enumerate(vals):
+        assert tuple(tr[o_qin + 2 * q:o_qin + 2 * q + 2]) == ini, (case["name"], q, "combineInitial")
+        assert tuple(tr[o_qfold + 2 * q:o_qfold + 2 * q + 2]) == fold, (case["name"], q, "folded")
+        assert tuple(tr[o_qfin + 2 * q:o_qfin + 2 * q + 2]) == fin, (case["name"], q, "final poly")
+
+
+def test_literal_transcript_and_fri_std_n12_two_folding_steps():
+    """The standard recursion shape (degree_bits 12: two arity-16 folds, a 16-coefficient final
+    polynomial), freshly generated: challenges and every per-query FRI value, literal vs oracle."""
+    from support import gen_circuit
+    gc = gen_circuit(12, 4, 0)
+    pj = gc.proof(1, 1)
+    common, vkey, pwpi = json.loads(gc.common), json.loads(gc.vkey), json.loads(pj)
+    ch = proof_challenges(common, vkey, pwpi)
+    st, tr = oracle().verify_json(gc.common, gc.vkey, pj, trace=True)
+    assert st == 1
+    tr = [int(x) for x in tr]
+    r, Q = common["config"]["num_challenges"], common["config"]["fri_config"]["num_query_rounds"]
+    S = len(pwpi["proof"]["opening_proof"]["commit_phase_merkle_caps"])
+    assert S == 2
+    o_qidx = 4 + 3 * r + 4 * r + 4 + 2 * S + 1
+    assert tr[o_qidx:o_qidx + Q] == ch["qidx"]
+    assert tr[4 + 3 * r + 4 * r:4 + 3 * r + 4 * r + 2] == ch["zeta"]
+    o_qin = o_qidx + Q + 4 * r
+    for q, (ini, fold, fin) in enumerate(fri_query_values(common, pwpi, ch)):
+        assert tuple(tr[o_qin + 2 * q:o_qin + 2 * q + 2]) == ini
+        assert tuple(tr[o_qin + 2 * Q + 2 * q:o_qin + 2 * Q + 2 * q + 2]) == fold
+        assert tuple(tr[o_qin + 4 * Q + 2 * q:o_qin + 4 * Q + 2 * q + 2]) == fin
+        assert fold == fin                          # round_ok for a valid proof
