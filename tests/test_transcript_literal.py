@@ -1,5 +1,5 @@
-"""A second, independent restatement of the Fiat-Shamir transcript and the FRI query rounds,
-checked against the oracle.
+"""A second, independent restatement of the Fiat-Shamir transcript, the FRI query rounds and
+the Plonk identity's permutation part, checked against the oracle.
 
 The oracle (oracle/oracle.c) and the GPU kernels share one author's reading of the reference.
 This file is a literal Python transliteration of the transcript, written clause by clause
@@ -403,3 +403,97 @@ def test_literal_transcript_and_fri_std_n12_two_folding_steps():
         assert tuple(tr[o_qin + 2 * Q + 2 * q:o_qin + 2 * Q + 2 * q + 2]) == fold
         assert tuple(tr[o_qin + 4 * Q + 2 * q:o_qin + 4 * Q + 2 * q + 2]) == fin
         assert fold == fin                          # round_ok for a valid proof
+    combined, quot = plonk_values(common, pwpi, ch)
+    o_comb = o_qidx + Q
+    assert [tuple(tr[o_comb + 2 * i:o_comb + 2 * i + 2]) for i in range(r)] == combined
+    assert [tuple(tr[o_comb + 2 * r + 2 * i:o_comb + 2 * r + 2 * i + 2]) for i in range(r)] == quot
+
+
+# ---------------------------------------------------------------------------------------------
+# The Plonk identity's permutation part, the same way: Plonk/Vanishing.hs:48-111 (zs1 and the
+# partial-product chunks, combined with powers of each alpha) and Plonk/Verifier.hs:35-51 (the
+# quotient chunks reduced in powers of zeta^n), for the circuits without lookups.  The
+# generator's gate filters are exactly 0 at zeta, so the gate terms add 0 and the
+# combined value is the permutation part alone; test_gpu covers the gate programs themselves
+# with every filter set to 1.
+
+def eval_lagrange0(nn, zeta):                       # Algebra/Poly.hs:14-17
+    if zeta == (1, 0):
+        return (1, 0)
+    return emul(esub(epow(zeta, nn), (1, 0)), einv(escale(nn % P, esub(zeta, (1, 0)))))
+
+
+def eprod(xs):
+    acc = (1, 0)
+    for x in xs:
+        acc = emul(acc, x)
+    return acc
+
+
+def chunks(k, xs):                                  # Misc/Aux.hs:110-113
+    return [xs[i:i + k] for i in range(0, len(xs), k)]
+
+
+def plonk_values(common, pwpi, ch):
+    """(combined C_i per challenge round, sum_k zeta^(nk) q_{i,k} per round)."""
+    cfg = common["config"]
+    r, qdf = cfg["num_challenges"], common["quotient_degree_factor"]
+    nn = 1 << common["fri_params"]["degree_bits"]
+    o = pwpi["proof"]["openings"]
+    ext = lambda xs: [(F(a), F(b)) for a, b in xs]
+    zeta = tuple(ch["zeta"])
+    zs, zs_next = ext(o["plonk_zs"]), ext(o["plonk_zs_next"])
+    wires, sigmas, pps = ext(o["wires"]), ext(o["plonk_sigmas"]), ext(o["partial_products"])
+    k_is = [F(k) for k in common["k_is"]]
+    zs1 = [emul(eval_lagrange0(nn, zeta), esub(z, (1, 0))) for z in zs]
+    pp_checks = []
+    for i, pp_chunk in enumerate(chunks(common["num_partial_products"], pps)[:r]):
+        beta, gamma = ch["betas"][i], ch["gammas"][i]
+        numers = chunks(qdf, [eadd(eadd(w, escale(fmul(beta, k), zeta)), (gamma, 0)) for k, w in zip(k_is, wires)])
+        denoms = chunks(qdf, [eadd(eadd(w, escale(beta, s)), (gamma, 0)) for s, w in zip(sigmas, wires)])
+        current = [zs[i]] + pp_chunk + [zs_next[i]]
+        prs = list(zip(current, current[1:]))     # Misc/Aux.hs:76-79
+        for (prev, nxt), nu, de in zip(prs, numers, denoms):
+            pp_checks.append(esub(emul(prev, eprod(nu)), emul(nxt, eprod(de))))
+    terms = zs1 + pp_checks                       # ++ lookup_checks (none) ++ gates (all 0 here)
+    combined = []
+    for a in ch["alphas"]:                        # combineWithPowersOfAlpha, Vanishing.hs:54-56
+        acc = (0, 0)
+        for x in reversed(terms):
+            acc = eadd(x, escale(a, acc))
+        combined.append(acc)
+    zeta_n = epow(zeta, nn)
+    quot = []
+    for chunk in chunks(qdf, ext(o["quotient_polys"])):   # Verifier.hs:43-49
+        acc = (0, 0)
+        for x in reversed(chunk):
+            acc = eadd(x, emul(zeta_n, acc))
+        quot.append(acc)
+    return combined, quot
+
+
+@pytest.mark.parametrize("idx", range(len(_fixtures()[0])))
+def test_literal_plonk_identity_values_match_oracle_trace(idx):
+    cases, rd = _fixtures()
+    case = cases[idx]
+    common_b, vkey_b = rd(case["circuit"] + "_common.json.gz"), rd(case["circuit"] + "_vkey.json.gz")
+    common = json.loads(common_b)
+    if common["num_lookup_polys"] > 0:
+        pytest.skip("lookup terms are not restated here")
+    proof_b = rd(case["name"] + "_proof.json.gz")
+    vkey, pwpi = json.loads(vkey_b), json.loads(proof_b)
+    ch = proof_challenges(common, vkey, pwpi)
+    combined, quot = plonk_values(common, pwpi, ch)
+    _, tr = oracle().verify_json(common_b, vkey_b, proof_b, trace=True)
+    tr = [int(x) for x in tr]
+    r = common["config"]["num_challenges"]
+    S = len(pwpi["proof"]["opening_proof"]["commit_phase_merkle_caps"])
+    Q = common["config"]["fri_config"]["num_query_rounds"]
+    o_comb = 4 + 3 * r + 4 * r + 4 + 2 * S + 1 + Q     # include/p2v.h trace layout
+    o_quot = o_comb + 2 * r
+    for i in range(r):
+        assert tuple(tr[o_comb + 2 * i:o_comb + 2 * i + 2]) == combined[i], (case["name"], i, "C_i")
+        assert tuple(tr[o_quot + 2 * i:o_quot + 2 * i + 2]) == quot[i], (case["name"], i, "quotient")
+    nn = 1 << common["fri_params"]["degree_bits"]
+    eqs_ok = all(emul(q, esub(epow(tuple(ch["zeta"]), nn), (1, 0))) == c for q, c in zip(quot, combined))
+    assert eqs_ok == bool(tr[o_quot + 2 * r + 6 * Q] & 1), case["name"]
