@@ -15,7 +15,7 @@
 #endif
 
 #ifndef P2V_MDS_BRANCH
-#define P2V_MDS_BRANCH 1   // MDS row reduction: the rare carry fix-up in a uniform branch
+#define P2V_MDS_BRANCH 2   // MDS row reduction: the rare carry fix-up in a uniform branch (1: per row, 2: per group of 4 rows)
 #endif
 #ifndef P2V_SBOX_MUL
 #define P2V_SBOX_MUL 2   // S-box multiply form (gl::mul_nc_dev_v): 2 = rare wrap as a uniform branch
@@ -214,6 +214,39 @@ __device__ __forceinline__ void mds_acc(const uint64_t* s, uint64_t& al, uint64_
     mds_acc<I, J + 1>(s, al, ah);
   }
 }
+#if P2V_MDS_BRANCH == 2
+// one row before its (rare) fix-up: r = t + ah_lo 2^32 with the carry-out mask c
+template <int I>
+__device__ __forceinline__ void row_unfixed(const uint64_t* s, const uint64_t* kl, const uint64_t* kh, uint64_t& r, uint64_t& c) {
+  using namespace gl::ax;
+  constexpr uint32_t C = mds_coeff(I, 0);
+  uint64_t al = madk_s<C>((uint32_t)s[0], kl[I]);
+  uint64_t ah = madk_s<C>((uint32_t)(s[0] >> 32), kh[I]);
+  mds_acc<I, 1>(s, al, ah);
+  uint64_t c0;
+  const uint64_t t = madm1_co((uint32_t)(ah >> 32), al, c0);   // < 2^45: no carry
+  const uint32_t rh = add_co((uint32_t)(t >> 32), (uint32_t)ah, c);
+  r = ((uint64_t)rh << 32) | (uint32_t)t;
+}
+// rows I..I+3 with one uniform branch for the group's fix-ups (one basic block per group, so
+// the compiler can batch the group's scalar constant loads)
+template <int I>
+__device__ __forceinline__ void mds_group(const uint64_t* s, uint64_t* t, const uint64_t* kl, const uint64_t* kh) {
+  using namespace gl::ax;
+  uint64_t r0, r1, r2, r3, c0, c1, c2, c3, d;
+  row_unfixed<I>(s, kl, kh, r0, c0);
+  row_unfixed<I + 1>(s, kl, kh, r1, c1);
+  row_unfixed<I + 2>(s, kl, kh, r2, c2);
+  row_unfixed<I + 3>(s, kl, kh, r3, c3);
+  if (__builtin_expect((c0 | c1 | c2 | c3) != 0, 0)) {
+    r0 = madm1_co(mask_1(c0), r0, d);
+    r1 = madm1_co(mask_1(c1), r1, d);
+    r2 = madm1_co(mask_1(c2), r2, d);
+    r3 = madm1_co(mask_1(c3), r3, d);
+  }
+  t[I] = r0; t[I + 1] = r1; t[I + 2] = r2; t[I + 3] = r3;
+}
+#endif
 // t[I..E) = (M s)[I..E) + k (k = the next round's constants, split into halves)
 template <int I, int E>
 __device__ __forceinline__ void mds_rows(const uint64_t* s, uint64_t* t, const uint64_t* kl, const uint64_t* kh) {
@@ -261,9 +294,15 @@ __device__ __forceinline__ void round_pp(uint64_t* s, uint64_t* t, int r, bool z
   }
   const uint64_t* kl = c_rc_split.lo + 12 * (r + 1);
   const uint64_t* kh = c_rc_split.hi + 12 * (r + 1);
+#if P2V_MDS_BRANCH == 2
+  if (g & 1) mds_group<0>(s, t, kl, kh);
+  if (g & 2) mds_group<4>(s, t, kl, kh);
+  if (g & 4) mds_group<8>(s, t, kl, kh);
+#else
   if (g & 1) mds_rows<0, 4>(s, t, kl, kh);
   if (g & 2) mds_rows<4, 8>(s, t, kl, kh);
   if (g & 4) mds_rows<8, 12>(s, t, kl, kh);
+#endif
 }
 }  // namespace dv
 
