@@ -15,7 +15,17 @@
 // commit-phase trees, final polynomial, proof-of-work grinding and query openings, all
 // following the verifier conventions of Plonk/FRI.hs and Challenge/*.hs.
 //
+// A second mode ("real", p2v_gen_circuit_new2) proves a genuine circuit instead: every gate
+// of the recursion gate set placed on rows, selector polynomials that pick each row's gate
+// (Gate/Selector.hs:83-95), gate constants per row, copy constraints with a real sigma
+// permutation, the running product Z and its partial products (Vanishing.hs:97-111), and the
+// quotient C(X)/Z_H(X) computed on a 16n-point coset and split into qdf chunks
+// (Verifier.hs:43-51).  Witness rows follow plonky2's gate semantics (gates.hpp), so every
+// vanishing term of a valid proof is a non-zero value at zeta.
+//
 // Exposed as a C ABI (libp2v_gen.so) for tests/ and bench.py.
+#include <algorithm>
+#include <thread>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -26,6 +36,7 @@
 #include <stdexcept>
 #include "../gl.h"
 #include "../poseidon.h"
+#include "gates.hpp"
 
 using gl::E;
 using u64 = uint64_t;
@@ -183,6 +194,8 @@ struct Circuit {
   int num_wires = 135, num_routed = 80, num_gate_consts = 2, r = 2, qdf = 8;
   int num_pis = 4;
   int ngroups = 3;
+  std::vector<int> grp_s, grp_e;   // selector groups [start, end) (SelectorsInfo, Types.hs:90-101)
+  u64 sel_fill = 0xFFFFFFFFULL;    // degenerate mode: the constant selector column value
   int nlp = 0;                 // num_lookup_polys (0 = no lookups)
   std::vector<std::vector<std::pair<u64, u64>>> luts;
   std::vector<std::string> gates;
@@ -200,6 +213,18 @@ struct Circuit {
   Tree const_tree;
   Digest circuit_digest;
   std::string common_json, vkey_json;
+  // ---- real mode
+  bool real = false;
+  int gate_set = 0;                                   // 0: recursion set, 1: small set (one selector group)
+  std::vector<gg::Gate> G;                            // gates in circuit order (ascending degree)
+  std::vector<int> row_gate;                          // [N]
+  std::vector<u64> row_consts;                        // [N][num_gate_consts]
+  std::vector<std::pair<int64_t, int64_t>> links;     // (dst, src) wire positions row*num_wires+wire, dst rows ascending
+  std::vector<std::vector<u64>> const_coeffs;         // constants-oracle columns as coefficient vectors
+  std::vector<std::vector<u64>> const_q;              // the same columns on the quotient coset (16N points)
+  std::vector<std::vector<u64>> const_h;              // the same columns on H (natural order)
+  int q_bits = 0;                                     // log2 of the quotient coset size
+  int max_constraints = 0;
 };
 
 std::string coset_gate_string(int bits) {
@@ -228,6 +253,187 @@ std::string keccak_str(u64 seed) {
   return s + "]";
 }
 
+// values on H = <omega> (natural order) -> coefficients
+std::vector<u64> interpolate(std::vector<u64> v, int lg) {
+  fft(v, lg, gl::inv(gl::subgroup_gen(lg)));
+  const u64 inv_n = gl::inv((u64)v.size());
+  for (auto& x : v) x = gl::mul(x, inv_n);
+  return v;
+}
+
+// rows of an oracle on the LDE coset g<eta>, bit-reversed order: rows[idx][col]
+std::vector<u64> oracle_rows(const std::vector<std::vector<u64>>& cols, int lde_bits) {
+  const size_t M = (size_t)1 << lde_bits, W = cols.size();
+  std::vector<u64> rows(M * W);
+  for (size_t c = 0; c < W; c++) {
+    auto l = lde(cols[c], lde_bits);
+    for (size_t idx = 0; idx < M; idx++) rows[idx * W + c] = l[gl::rev_bits(lde_bits, (uint32_t)idx)];
+  }
+  return rows;
+}
+
+template <class Fn> void parallel_for(size_t n, Fn fn) {
+  unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (n < 64) nt = 1;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; t++) th.emplace_back([&, t] { for (size_t i = t; i < n; i += nt) fn(i); });
+  for (auto& x : th) x.join();
+}
+
+gg::Gate mkgate(gg::Kind k, int64_t p0, int64_t p1, int64_t p2, std::string str) {
+  gg::Gate g; g.kind = k; g.p0 = p0; g.p1 = p1; g.p2 = p2; g.str = std::move(str); return g;
+}
+
+// total degree of a gate's constraints in the wires and constants: evaluate along a random
+// line (w = a + t b) and read off the degree in t from forward differences
+int measure_degree(const gg::Gate& g, int nw, int nk, Rng& rg) {
+  const int D = 12;
+  std::vector<u64> a(nw), b(nw), ka(nk), kb(nk), pih(4);
+  for (auto& x : a) x = rg.field();
+  for (auto& x : b) x = rg.field();
+  for (auto& x : ka) x = rg.field();
+  for (auto& x : kb) x = rg.field();
+  for (auto& x : pih) x = rg.field();
+  std::vector<std::vector<u64>> vals;
+  std::vector<u64> w(nw), k(nk);
+  for (int t = 0; t < D; t++) {
+    for (int i = 0; i < nw; i++) w[i] = gl::add(a[i], gl::mul((u64)t, b[i]));
+    for (int i = 0; i < nk; i++) k[i] = gl::add(ka[i], gl::mul((u64)t, kb[i]));
+    std::vector<u64> out;
+    gg::eval(g, w.data(), nw, k.data(), nk, pih.data(), out);
+    vals.push_back(std::move(out));
+  }
+  int deg = 0;
+  for (size_t c = 0; c < vals[0].size(); c++) {
+    std::vector<u64> d(D);
+    for (int t = 0; t < D; t++) d[t] = vals[t][c];
+    int dc = -1;
+    for (int m = 0; m < D; m++) {   // d holds the m-th differences
+      for (int t = 0; t + m < D; t++) if (d[t] != 0) { dc = m; break; }
+      for (int t = 0; t + m + 1 < D; t++) d[t] = gl::sub(d[t + 1], d[t]);
+    }
+    if (dc >= D - 2) throw std::runtime_error("gen: constraint degree too high to measure");
+    deg = std::max(deg, dc);
+  }
+  return deg;
+}
+
+void build_real(Circuit& C) {
+  if (!C.luts.empty()) throw std::runtime_error("gen: real mode has no lookup argument prover");
+  const int N = C.N, NW = C.num_wires, NR = C.num_routed, NK = C.num_gate_consts;
+  Rng rg(C.circuit_seed * 7919 + 17);
+  for (int i = 0; i < 4; i++) C.circuit_digest.e[i] = rg.field();
+  const std::string PH = "_phantom: PhantomData<plonky2_field::goldilocks_field::GoldilocksField>";
+  using namespace gg;
+  if (C.gate_set == 1) {
+    C.G = { mkgate(NOOP, 0, 0, 0, "NoopGate"), mkgate(CONST, 2, 0, 0, "ConstantGate { num_consts: 2 }"),
+            mkgate(PI, 0, 0, 0, "PublicInputGate"), mkgate(ARITH, 20, 0, 0, "ArithmeticGate { num_ops: 20 }") };
+  } else {
+    C.G = {
+      mkgate(NOOP, 0, 0, 0, "NoopGate"),
+      mkgate(CONST, 2, 0, 0, "ConstantGate { num_consts: 2 }"),
+      mkgate(POSEIDON_MDS, 12, 0, 0, "PoseidonMdsGate(PhantomData<plonky2_field::goldilocks_field::GoldilocksField>)<WIDTH=12>"),
+      mkgate(PI, 0, 0, 0, "PublicInputGate"),
+      mkgate(BASESUM, 63, 2, 0, "BaseSumGate { num_limbs: 63 } + Base: 2"),
+      mkgate(REDUCING_EXT, 32, 0, 0, "ReducingExtensionGate { num_coeffs: 32 }"),
+      mkgate(REDUCING, 43, 0, 0, "ReducingGate { num_coeffs: 43 }"),
+      mkgate(ARITH_EXT, 10, 0, 0, "ArithmeticExtensionGate { num_ops: 10 }"),
+      mkgate(ARITH, 20, 0, 0, "ArithmeticGate { num_ops: 20 }"),
+      mkgate(MULEXT, 13, 0, 0, "MulExtensionGate { num_ops: 13 }"),
+      mkgate(RANDACC, 4, 4, 2, "RandomAccessGate { bits: 4, num_copies: 4, num_extra_constants: 2, " + PH + " }<D=2>"),
+      mkgate(EXP, 66, 0, 0, "ExponentiationGate { num_power_bits: 66 }"),
+      mkgate(COSET, 4, 6, 0, coset_gate_string(4)),
+      mkgate(POSEIDON, 12, 0, 0, "PoseidonGate(PhantomData<plonky2_field::goldilocks_field::GoldilocksField>)<WIDTH=12>"),
+    };
+    auto& cg = C.G[12];   // the barycentric weights, as the gate string carries them
+    const int n = 16; const u64 gsub = gl::subgroup_gen(4);
+    std::vector<u64> pts(n); pts[0] = 1; for (int i = 1; i < n; i++) pts[i] = gl::mul(pts[i - 1], gsub);
+    for (int i = 0; i < n; i++) { u64 pr = 1; for (int j = 0; j < n; j++) if (j != i) pr = gl::mul(pr, gl::sub(pts[i], pts[j])); cg.weights.push_back(gl::inv(pr)); }
+  }
+  // degrees, sorted ascending (plonky2 orders a circuit's gates by degree), selector groups:
+  // one group if max_deg + #gates - 1 <= qdf, else greedy ranges with size + degree <= qdf
+  Rng drg(99);
+  for (auto& g : C.G) g.degree = measure_degree(g, NW, NK, drg);
+  std::stable_sort(C.G.begin(), C.G.end(), [](const gg::Gate& x, const gg::Gate& y) { return x.degree < y.degree; });
+  const int NG = (int)C.G.size();
+  C.gates.clear();
+  for (auto& g : C.G) C.gates.push_back(g.str);
+  C.grp_s.clear(); C.grp_e.clear();
+  if (C.G.back().degree + NG - 1 <= C.qdf) { C.grp_s = {0}; C.grp_e = {NG}; }
+  else {
+    for (int st = 0; st < NG;) {
+      int sz = 0;
+      while (st + sz < NG && sz + C.G[st + sz].degree < C.qdf) sz++;
+      if (sz == 0) throw std::runtime_error("gen: a gate's degree exceeds the quotient degree");
+      C.grp_s.push_back(st); C.grp_e.push_back(st + sz); st += sz;
+    }
+  }
+  C.ngroups = (int)C.grp_s.size();
+  C.sel_idx.assign(NG, 0);
+  for (int g = 0; g < C.ngroups; g++) for (int k = C.grp_s[g]; k < C.grp_e[g]; k++) C.sel_idx[k] = g;
+  C.num_constants = C.ngroups + C.nls + NK;
+  C.max_constraints = 0;
+  {
+    std::vector<u64> w(NW, 1), k(NK, 1), pih(4, 0), out;
+    for (auto& g : C.G) { out.clear(); gg::eval(g, w.data(), NW, k.data(), NK, pih.data(), out); C.max_constraints = std::max(C.max_constraints, (int)out.size()); }
+  }
+  C.num_gate_constraints = C.max_constraints;
+  // rows: every gate once, then random gates; row constants random where the gate reads them
+  C.row_gate.assign(N, 0);
+  for (int i = 0; i < N; i++) C.row_gate[i] = i < NG ? i : (int)(rg.next() % (u64)NG);
+  C.row_consts.assign((size_t)N * NK, 0);
+  for (int i = 0; i < N; i++) {
+    int nc = gg::num_row_constants(C.G[C.row_gate[i]]);
+    if (nc > NK) throw std::runtime_error("gen: gate needs more constants than the config has");
+    for (int c = 0; c < nc; c++) C.row_consts[(size_t)i * NK + c] = rg.field();
+  }
+  // copy constraints: a free routed input of a later row copies any routed wire of an earlier row
+  C.links.clear();
+  for (int i = 1; i < N; i++)
+    for (int wi : gg::free_inputs(C.G[C.row_gate[i]], NW)) {
+      if (wi >= NR || rg.next() % 6 != 0) continue;
+      const int64_t src = (int64_t)(rg.next() % (u64)i) * NW + (int64_t)(rg.next() % (u64)NR);
+      C.links.push_back({(int64_t)i * NW + wi, src});
+    }
+  // sigma: the copy classes (union-find over routed positions j*N + i) as cycles in position order
+  const size_t NP = (size_t)NR * N;
+  std::vector<uint32_t> par(NP);
+  for (size_t p = 0; p < NP; p++) par[p] = (uint32_t)p;
+  auto find = [&](uint32_t x) { while (par[x] != x) { par[x] = par[par[x]]; x = par[x]; } return x; };
+  auto rpos = [&](int64_t wp) { return (uint32_t)((wp % NW) * N + wp / NW); };
+  for (auto& l : C.links) { uint32_t a = find(rpos(l.first)), b = find(rpos(l.second)); if (a != b) par[std::max(a, b)] = std::min(a, b); }
+  std::vector<uint32_t> sigma(NP), last(NP, UINT32_MAX), first(NP, UINT32_MAX);
+  for (size_t p = 0; p < NP; p++) {
+    uint32_t r = find((uint32_t)p);
+    if (first[r] == UINT32_MAX) first[r] = (uint32_t)p; else sigma[last[r]] = (uint32_t)p;
+    last[r] = (uint32_t)p;
+  }
+  for (size_t p = 0; p < NP; p++) if (find((uint32_t)p) == p) sigma[last[p]] = first[p];
+  // constant columns on H: [selectors | gate constants | sigmas]
+  const u64 omega = gl::subgroup_gen(C.degree_bits);
+  std::vector<u64> om(N); om[0] = 1; for (int i = 1; i < N; i++) om[i] = gl::mul(om[i - 1], omega);
+  std::vector<std::vector<u64>> cols;
+  for (int g = 0; g < C.ngroups; g++) {
+    std::vector<u64> v(N);
+    for (int i = 0; i < N; i++) { int k = C.row_gate[i]; v[i] = C.sel_idx[k] == g ? (u64)k : 0xFFFFFFFFULL; }
+    cols.push_back(std::move(v));
+  }
+  for (int c = 0; c < NK; c++) { std::vector<u64> v(N); for (int i = 0; i < N; i++) v[i] = C.row_consts[(size_t)i * NK + c]; cols.push_back(std::move(v)); }
+  for (int j = 0; j < NR; j++) {
+    std::vector<u64> v(N);
+    for (int i = 0; i < N; i++) { uint32_t t = sigma[(size_t)j * N + i]; v[i] = gl::mul(C.k_is[t / N], om[t % N]); }
+    cols.push_back(std::move(v));
+  }
+  C.const_width = (int)cols.size();
+  C.const_h = cols;
+  C.const_coeffs.resize(cols.size());
+  parallel_for(cols.size(), [&](size_t c) { C.const_coeffs[c] = interpolate(cols[c], C.degree_bits); });
+  C.const_lde = oracle_rows(C.const_coeffs, C.lde_bits);
+  C.q_bits = C.degree_bits + 4;   // >= (qdf + 1) n points
+  C.const_q.resize(cols.size());
+  parallel_for(cols.size(), [&](size_t c) { C.const_q[c] = lde(C.const_coeffs[c], C.q_bits); });
+}
+
 void build_circuit(Circuit& C) {
   C.N = 1 << C.degree_bits;
   C.lde_bits = C.degree_bits + C.rate_bits;
@@ -236,62 +442,75 @@ void build_circuit(Circuit& C) {
   C.npp = (C.num_routed + C.qdf - 1) / C.qdf - 1;
   C.arities.clear();
   for (int logn = C.degree_bits; logn > C.final_poly_bits; logn -= C.arity_bits) C.arities.push_back(C.arity_bits);
-  if (C.gates.empty()) {
-    C.gates = {
-      "NoopGate",
-      "ConstantGate { num_consts: 2 }",
-      "PoseidonMdsGate(PhantomData<plonky2_field::goldilocks_field::GoldilocksField>)<WIDTH=12>",
-      "PublicInputGate",
-      "BaseSumGate { num_limbs: 63 } + Base: 2",
-      "ReducingExtensionGate { num_coeffs: 32 }",
-      "ReducingGate { num_coeffs: 43 }",
-      "ArithmeticExtensionGate { num_ops: 10 }",
-      "ArithmeticGate { num_ops: 20 }",
-      "MulExtensionGate { num_ops: 13 }",
-      "RandomAccessGate { bits: 4, num_copies: 4, num_extra_constants: 2, _phantom: PhantomData<plonky2_field::goldilocks_field::GoldilocksField> }<D=2>",
-      "ExponentiationGate { num_power_bits: 66 }",
-      coset_gate_string(4),
-      "PoseidonGate(PhantomData<plonky2_field::goldilocks_field::GoldilocksField>)<WIDTH=12>",
-    };
-    if (!C.luts.empty()) {
-      for (size_t t = 0; t < C.luts.size(); t++) {
-        C.gates.insert(C.gates.begin() + 1, "LookupTableGate { num_slots: 26, lut_hash: " + keccak_str(100 + t) +
-                                               ", last_lut_row: " + std::to_string((C.luts[t].size() + 25) / 26) + " }");
-        C.gates.insert(C.gates.begin() + 1, "LookupGate { num_slots: 40, lut_hash: " + keccak_str(100 + t) + " }");
-      }
-    }
-  }
-  C.sel_idx.assign(C.gates.size(), 0);
-  {  // split gates into ngroups contiguous groups
-    size_t per = (C.gates.size() + C.ngroups - 1) / C.ngroups;
-    for (size_t g = 0; g < C.gates.size(); g++) C.sel_idx[g] = (int)(g / per);
-    C.ngroups = C.sel_idx.back() + 1;
-    C.num_constants = C.ngroups + C.nls + C.num_gate_consts;
-  }
   C.k_is.resize(C.num_routed);
   { u64 k = 1; for (int i = 0; i < C.num_routed; i++) { C.k_is[i] = k; k = gl::mul(k, gl::MULT_GEN); } }
-
-  Rng rg(C.circuit_seed * 7919 + 17);
-  C.gate_const_coeffs.assign(C.num_gate_consts, std::vector<u64>(C.N));
-  for (auto& p : C.gate_const_coeffs) for (auto& c : p) c = rg.field();
-  for (int i = 0; i < 4; i++) C.circuit_digest.e[i] = rg.field();
-
-  // constants oracle: [selectors (UNUSED) | lookup selectors (0) | gate constants | sigmas]
   size_t M = (size_t)1 << C.lde_bits;
-  C.const_width = C.num_constants + C.num_routed;
-  C.const_lde.assign(M * C.const_width, 0);
-  std::vector<std::vector<u64>> gc_lde;
-  for (auto& p : C.gate_const_coeffs) gc_lde.push_back(lde(p, C.lde_bits));
-  u64 eta = gl::subgroup_gen(C.lde_bits);
-  std::vector<u64> xs(M); { u64 x = gl::MULT_GEN; for (size_t i = 0; i < M; i++) { xs[i] = x; x = gl::mul(x, eta); } }
-  for (size_t idx = 0; idx < M; idx++) {
-    size_t nat = gl::rev_bits(C.lde_bits, (uint32_t)idx);
-    u64* row = &C.const_lde[idx * C.const_width];
-    int c = 0;
-    for (int g = 0; g < C.ngroups; g++) row[c++] = 0xFFFFFFFFULL;
-    for (int g = 0; g < C.nls; g++) row[c++] = 0;
-    for (int g = 0; g < C.num_gate_consts; g++) row[c++] = gc_lde[g][nat];
-    for (int j = 0; j < C.num_routed; j++) row[c++] = gl::mul(C.k_is[j], xs[nat]);
+  if (C.real) build_real(C);
+  else {
+    if (C.gates.empty()) {
+      C.gates = {
+        "NoopGate",
+        "ConstantGate { num_consts: 2 }",
+        "PoseidonMdsGate(PhantomData<plonky2_field::goldilocks_field::GoldilocksField>)<WIDTH=12>",
+        "PublicInputGate",
+        "BaseSumGate { num_limbs: 63 } + Base: 2",
+        "ReducingExtensionGate { num_coeffs: 32 }",
+        "ReducingGate { num_coeffs: 43 }",
+        "ArithmeticExtensionGate { num_ops: 10 }",
+        "ArithmeticGate { num_ops: 20 }",
+        "MulExtensionGate { num_ops: 13 }",
+        "RandomAccessGate { bits: 4, num_copies: 4, num_extra_constants: 2, _phantom: PhantomData<plonky2_field::goldilocks_field::GoldilocksField> }<D=2>",
+        "ExponentiationGate { num_power_bits: 66 }",
+        coset_gate_string(4),
+        "PoseidonGate(PhantomData<plonky2_field::goldilocks_field::GoldilocksField>)<WIDTH=12>",
+      };
+      if (!C.luts.empty()) {
+        for (size_t t = 0; t < C.luts.size(); t++) {
+          C.gates.insert(C.gates.begin() + 1, "LookupTableGate { num_slots: 26, lut_hash: " + keccak_str(100 + t) +
+                                                 ", last_lut_row: " + std::to_string((C.luts[t].size() + 25) / 26) + " }");
+          C.gates.insert(C.gates.begin() + 1, "LookupGate { num_slots: 40, lut_hash: " + keccak_str(100 + t) + " }");
+        }
+      }
+    }
+    C.sel_idx.assign(C.gates.size(), 0);
+    {  // split gates into ngroups contiguous groups
+      size_t per = (C.gates.size() + C.ngroups - 1) / C.ngroups;
+      for (size_t g = 0; g < C.gates.size(); g++) C.sel_idx[g] = (int)(g / per);
+      C.ngroups = C.sel_idx.back() + 1;
+      C.num_constants = C.ngroups + C.nls + C.num_gate_consts;
+      C.grp_s.clear(); C.grp_e.clear();
+      for (int g = 0; g < C.ngroups; g++) { C.grp_s.push_back((int)(g * per)); C.grp_e.push_back((int)std::min(C.gates.size(), (size_t)(g + 1) * per)); }
+    }
+    // every gate filter must be 0 at every point: with several groups the UNUSED factor does
+    // it; with one group the selector column is NoopGate's index (its filter is the only
+    // non-zero one, and NoopGate has no constraints)
+    C.sel_fill = 0xFFFFFFFFULL;
+    if (C.ngroups == 1) {
+      auto it = std::find(C.gates.begin(), C.gates.end(), std::string("NoopGate"));
+      if (it == C.gates.end()) throw std::runtime_error("gen: one selector group needs a NoopGate");
+      C.sel_fill = (u64)(it - C.gates.begin());
+    }
+    Rng rg(C.circuit_seed * 7919 + 17);
+    C.gate_const_coeffs.assign(C.num_gate_consts, std::vector<u64>(C.N));
+    for (auto& p : C.gate_const_coeffs) for (auto& c : p) c = rg.field();
+    for (int i = 0; i < 4; i++) C.circuit_digest.e[i] = rg.field();
+
+    // constants oracle: [selectors (UNUSED) | lookup selectors (0) | gate constants | sigmas]
+    C.const_width = C.num_constants + C.num_routed;
+    C.const_lde.assign(M * C.const_width, 0);
+    std::vector<std::vector<u64>> gc_lde;
+    for (auto& p : C.gate_const_coeffs) gc_lde.push_back(lde(p, C.lde_bits));
+    u64 eta = gl::subgroup_gen(C.lde_bits);
+    std::vector<u64> xs(M); { u64 x = gl::MULT_GEN; for (size_t i = 0; i < M; i++) { xs[i] = x; x = gl::mul(x, eta); } }
+    for (size_t idx = 0; idx < M; idx++) {
+      size_t nat = gl::rev_bits(C.lde_bits, (uint32_t)idx);
+      u64* row = &C.const_lde[idx * C.const_width];
+      int c = 0;
+      for (int g = 0; g < C.ngroups; g++) row[c++] = C.sel_fill;
+      for (int g = 0; g < C.nls; g++) row[c++] = 0;
+      for (int g = 0; g < C.num_gate_consts; g++) row[c++] = gc_lde[g][nat];
+      for (int j = 0; j < C.num_routed; j++) row[c++] = gl::mul(C.k_is[j], xs[nat]);
+    }
   }
   std::vector<Digest> leaves(M);
   for (size_t idx = 0; idx < M; idx++) sponge(&C.const_lde[idx * C.const_width], C.const_width, leaves[idx].e);
@@ -316,13 +535,9 @@ void build_circuit(Circuit& C) {
   j.raw("],\"selectors_info\":{\"selector_indices\":[");
   for (size_t g = 0; g < C.sel_idx.size(); g++) { if (g) j.raw(","); j.i(C.sel_idx[g]); }
   j.raw("],\"groups\":[");
-  {
-    size_t per = (C.gates.size() + C.ngroups - 1) / C.ngroups;
-    for (int g = 0; g < C.ngroups; g++) {
-      if (g) j.raw(",");
-      size_t s = g * per, e = std::min(C.gates.size(), (size_t)(g + 1) * per);
-      j.raw("{\"start\":"); j.i((long long)s); j.raw(",\"end\":"); j.i((long long)e); j.raw("}");
-    }
+  for (int g = 0; g < C.ngroups; g++) {
+    if (g) j.raw(",");
+    j.raw("{\"start\":"); j.i(C.grp_s[g]); j.raw(",\"end\":"); j.i(C.grp_e[g]); j.raw("}");
   }
   j.raw("]},\"quotient_degree_factor\":"); j.i(C.qdf);
   j.raw(",\"num_gate_constraints\":"); j.i(C.num_gate_constraints);
@@ -355,7 +570,177 @@ struct Witness {
   std::vector<u64> q_lde;                        // [M][r*qdf] (all zero)
   int zw = 0, qw = 0;
   Tree wires_tree, zs_tree, q_tree;
+  // real mode
+  std::vector<u64> pis;                          // public inputs (fixed by the witness: PublicInputGate)
+  std::vector<std::vector<u64>> zs_coeffs;       // [r*(1+npp)] Z_j, then the partial products
+  std::vector<std::vector<u64>> q_coeffs;        // [r*qdf] quotient chunks
 };
+
+void tree_of_rows(const std::vector<u64>& rows, int width, int lde_bits, int cap_height, Tree& t) {
+  const size_t M = (size_t)1 << lde_bits;
+  std::vector<Digest> leaves(M);
+  parallel_for(M, [&](size_t idx) { sponge(&rows[idx * width], width, leaves[idx].e); });
+  t.build(std::move(leaves), lde_bits, cap_height);
+}
+
+void batch_inv_base(std::vector<u64>& v) {   // Montgomery's trick over F (no zeros expected)
+  const size_t n = v.size();
+  std::vector<u64> pre(n);
+  u64 acc = 1;
+  for (size_t i = 0; i < n; i++) { pre[i] = acc; acc = gl::mul(acc, v[i]); }
+  if (acc == 0) throw std::runtime_error("gen: zero in a batch inversion");
+  u64 inv = gl::inv(acc);
+  for (size_t i = n; i-- > 0;) { u64 t = gl::mul(inv, pre[i]); inv = gl::mul(inv, v[i]); v[i] = t; }
+}
+
+// A real witness and the prover's first three rounds (Plonky2's order: wires, then Z/partial
+// products after beta/gamma, then the quotient after alpha), reproducing the verifier's
+// transcript (Challenge/Verifier.hs:58-92).
+Witness* make_witness_real(const Circuit& C, u64 seed) {
+  auto* W = new Witness();
+  Rng rg(seed * 1000003 + 11);
+  const int N = C.N, NW = C.num_wires, NR = C.num_routed, NK = C.num_gate_consts, r = C.r, n = C.degree_bits;
+  W->pis.resize(C.num_pis);
+  for (auto& x : W->pis) x = rg.field();
+  u64 pih[4] = {0, 0, 0, 0};
+  if (!W->pis.empty()) sponge(W->pis.data(), W->pis.size(), pih);
+  // ---- wires: rows in order; a copy constraint presets its (free input) destination
+  std::vector<u64> rows((size_t)N * NW);
+  std::vector<uint8_t> pre(NW);
+  gg::Rng wrg(seed * 7 + 3);
+  size_t li = 0;
+  std::vector<u64> out;
+  for (int i = 0; i < N; i++) {
+    std::fill(pre.begin(), pre.end(), 0);
+    u64* w = &rows[(size_t)i * NW];
+    for (; li < C.links.size() && C.links[li].first / NW == i; li++) {
+      const int wi = (int)(C.links[li].first % NW);
+      w[wi] = rows[C.links[li].second]; pre[wi] = 1;
+    }
+    const gg::Gate& g = C.G[C.row_gate[i]];
+    const u64* k = &C.row_consts[(size_t)i * NK];
+    gg::fill(g, w, pre.data(), NW, k, pih, wrg);
+    out.clear();
+    gg::eval(g, w, NW, k, NK, pih, out);
+    for (size_t t = 0; t < out.size(); t++)
+      if (out[t]) throw std::runtime_error("gen: witness row " + std::to_string(i) + " violates constraint " + std::to_string(t) + " of " + g.str);
+  }
+  W->wire_coeffs.resize(NW);
+  parallel_for(NW, [&](size_t c) {
+    std::vector<u64> v(N);
+    for (int i = 0; i < N; i++) v[i] = rows[(size_t)i * NW + c];
+    W->wire_coeffs[c] = interpolate(std::move(v), n);
+  });
+  W->wires_lde = oracle_rows(W->wire_coeffs, C.lde_bits);
+  tree_of_rows(W->wires_lde, NW, C.lde_bits, C.cap_height, W->wires_tree);
+  Duplex d;
+  for (int i = 0; i < 4; i++) d.absorb(C.circuit_digest.e[i]);
+  for (int i = 0; i < 4; i++) d.absorb(pih[i]);
+  d.absorb_digests(W->wires_tree.cap());
+  std::vector<u64> betas(r), gammas(r), alphas(r);
+  for (auto& b : betas) b = d.squeeze();
+  for (auto& g : gammas) g = d.squeeze();
+  // ---- Z and the partial products per challenge round (Vanishing.hs:97-111)
+  const int nch = (NR + C.qdf - 1) / C.qdf;   // chunks; partial products = nch - 1 = npp
+  const u64 omega = gl::subgroup_gen(n);
+  std::vector<u64> om(N); om[0] = 1; for (int i = 1; i < N; i++) om[i] = gl::mul(om[i - 1], omega);
+  W->zw = r * (1 + C.npp);
+  std::vector<std::vector<u64>> zcols(W->zw, std::vector<u64>(N));
+  for (int j = 0; j < r; j++) {
+    std::vector<u64> num((size_t)N * nch), den((size_t)N * nch);
+    parallel_for(N, [&](size_t i) {
+      for (int c = 0; c < nch; c++) {
+        u64 pn = 1, pd = 1;
+        for (int t = c * C.qdf; t < NR && t < (c + 1) * C.qdf; t++) {
+          const u64 w = rows[i * NW + t];
+          pn = gl::mul(pn, gl::add(gl::add(w, gl::mul(betas[j], gl::mul(C.k_is[t], om[i]))), gammas[j]));
+          pd = gl::mul(pd, gl::add(gl::add(w, gl::mul(betas[j], C.const_h[C.ngroups + NK + t][i])), gammas[j]));
+        }
+        num[i * nch + c] = pn; den[i * nch + c] = pd;
+      }
+    });
+    batch_inv_base(den);
+    u64 z = 1;
+    for (int i = 0; i < N; i++) {
+      zcols[j][i] = z;
+      u64 cur = z;
+      for (int c = 0; c < nch; c++) {
+        cur = gl::mul(cur, gl::mul(num[(size_t)i * nch + c], den[(size_t)i * nch + c]));
+        if (c < nch - 1) zcols[r + j * C.npp + c][i] = cur;
+      }
+      z = cur;
+    }
+    if (z != 1) throw std::runtime_error("gen: the permutation product is not 1 (copy constraints violated)");
+  }
+  W->zs_coeffs.resize(W->zw);
+  parallel_for(W->zw, [&](size_t c) { W->zs_coeffs[c] = interpolate(zcols[c], n); });
+  W->zs_lde = oracle_rows(W->zs_coeffs, C.lde_bits);
+  tree_of_rows(W->zs_lde, W->zw, C.lde_bits, C.cap_height, W->zs_tree);
+  d.absorb_digests(W->zs_tree.cap());
+  for (auto& a : alphas) a = d.squeeze();
+  // ---- the quotient: C_i(x) / (x^n - 1) on g<nu>, |<nu>| = 2^q_bits >= (qdf + 1) n
+  const int qb = C.q_bits;
+  const size_t MQ = (size_t)1 << qb, shift = MQ / (size_t)N;   // omega = nu^shift
+  std::vector<std::vector<u64>> wq(NW), zq(W->zw);
+  parallel_for(NW, [&](size_t c) { wq[c] = lde(W->wire_coeffs[c], qb); });
+  parallel_for(W->zw, [&](size_t c) { zq[c] = lde(W->zs_coeffs[c], qb); });
+  const u64 nu = gl::subgroup_gen(qb);
+  const int NG = (int)C.G.size(), TG = C.max_constraints;
+  std::vector<std::vector<u64>> qv(r, std::vector<u64>(MQ));
+  parallel_for(MQ, [&](size_t t) {
+    const u64 x = gl::mul(gl::MULT_GEN, gl::pow(nu, t));
+    const u64 zh = gl::sub(gl::pow(x, (u64)N), 1);
+    const u64 L0 = gl::mul(zh, gl::inv(gl::mul((u64)N % gl::P, gl::sub(x, 1))));
+    std::vector<u64> terms;
+    for (int j = 0; j < r; j++) terms.push_back(gl::mul(L0, gl::sub(zq[j][t], 1)));
+    for (int j = 0; j < r; j++) {
+      for (int c = 0; c < nch; c++) {
+        const u64 prev = c == 0 ? zq[j][t] : zq[r + j * C.npp + c - 1][t];
+        const u64 next = c == nch - 1 ? zq[j][(t + shift) % MQ] : zq[r + j * C.npp + c][t];
+        u64 pn = 1, pd = 1;
+        for (int s = c * C.qdf; s < NR && s < (c + 1) * C.qdf; s++) {
+          pn = gl::mul(pn, gl::add(gl::add(wq[s][t], gl::mul(gl::mul(betas[j], C.k_is[s]), x)), gammas[j]));
+          pd = gl::mul(pd, gl::add(gl::add(wq[s][t], gl::mul(betas[j], C.const_q[C.ngroups + NK + s][t])), gammas[j]));
+        }
+        terms.push_back(gl::sub(gl::mul(prev, pn), gl::mul(next, pd)));
+      }
+    }
+    std::vector<u64> wv(NW), kv(NK), cons, vsum(TG, 0);
+    for (int c = 0; c < NW; c++) wv[c] = wq[c][t];
+    for (int c = 0; c < NK; c++) kv[c] = C.const_q[C.ngroups + c][t];
+    for (int k = 0; k < NG; k++) {
+      const int g = C.sel_idx[k];
+      const u64 S = C.const_q[g][t];
+      u64 filt = C.ngroups > 1 ? gl::sub(0xFFFFFFFFULL, S) : 1;   // Gate/Selector.hs:83-89
+      for (int m = C.grp_s[g]; m < C.grp_e[g]; m++) if (m != k) filt = gl::mul(filt, gl::sub((u64)m, S));
+      cons.clear();
+      gg::eval(C.G[k], wv.data(), NW, kv.data(), NK, pih, cons);
+      for (size_t q = 0; q < cons.size(); q++) vsum[q] = gl::add(vsum[q], gl::mul(filt, cons[q]));
+    }
+    terms.insert(terms.end(), vsum.begin(), vsum.end());
+    const u64 izh = gl::inv(zh);
+    for (int i = 0; i < r; i++) {
+      u64 acc = 0;   // sum_s alpha^s term_s (Vanishing.hs:54-56)
+      for (size_t s = terms.size(); s-- > 0;) acc = gl::add(terms[s], gl::mul(alphas[i], acc));
+      qv[i][t] = gl::mul(acc, izh);
+    }
+  });
+  W->qw = r * C.qdf;
+  W->q_coeffs.assign(W->qw, std::vector<u64>(N));
+  const u64 ginv = gl::inv(gl::MULT_GEN);
+  for (int i = 0; i < r; i++) {
+    auto co = interpolate(qv[i], qb);   // coefficients of Q(g y); Q's m-th is co[m] g^-m
+    u64 gp = 1;
+    for (size_t m = 0; m < MQ; m++, gp = gl::mul(gp, ginv)) {
+      const u64 qm = gl::mul(co[m], gp);
+      if (m < (size_t)C.qdf * N) W->q_coeffs[i * C.qdf + m / N][m % N] = qm;
+      else if (qm != 0) throw std::runtime_error("gen: the constraint polynomial does not vanish on H (quotient degree too high)");
+    }
+  }
+  W->q_lde = oracle_rows(W->q_coeffs, C.lde_bits);
+  tree_of_rows(W->q_lde, W->qw, C.lde_bits, C.cap_height, W->q_tree);
+  return W;
+}
 
 Witness* make_witness(const Circuit& C, u64 seed) {
   auto* W = new Witness();
@@ -402,7 +787,8 @@ std::string make_proof(const Circuit& C, const Witness& W, u64 pi_seed, unsigned
   const size_t M = (size_t)1 << C.lde_bits;
   const int r = C.r;
   std::vector<u64> pis(C.num_pis);
-  for (auto& x : pis) x = rg.field();
+  if (C.real) pis = W.pis;
+  else for (auto& x : pis) x = rg.field();
   u64 pih[4]; sponge(pis.data(), pis.size(), pih);
   if (pis.empty()) memset(pih, 0, sizeof pih);
 
@@ -423,15 +809,25 @@ std::string make_proof(const Circuit& C, const Witness& W, u64 pi_seed, unsigned
 
   // openings at zeta (OpeningSet order, Types.hs:265-279)
   std::vector<E> o_const, o_sig, o_wires, o_zs, o_zs_next, o_pp, o_quot, o_lzs, o_lzs_next;
-  for (int g = 0; g < C.ngroups; g++) o_const.push_back(gl::eb(0xFFFFFFFFULL));
-  for (int g = 0; g < C.nls; g++) o_const.push_back(gl::e0());
-  for (int g = 0; g < C.num_gate_consts; g++) o_const.push_back(eval_at(C.gate_const_coeffs[g], zeta));
-  for (int j = 0; j < C.num_routed; j++) o_sig.push_back(gl::escale(C.k_is[j], zeta));
-  for (int w = 0; w < C.num_wires; w++) o_wires.push_back(eval_at(W.wire_coeffs[w], zeta));
-  for (int i = 0; i < r; i++) { o_zs.push_back(gl::eb(1)); o_zs_next.push_back(gl::eb(1)); }
-  for (int i = 0; i < r * C.npp; i++) o_pp.push_back(gl::eb(1));
-  for (int i = 0; i < r * C.qdf; i++) o_quot.push_back(gl::e0());
-  if (flags & 4) o_quot[0] = gl::eb(12345);
+  if (C.real) {
+    for (int c = 0; c < C.num_constants; c++) o_const.push_back(eval_at(C.const_coeffs[c], zeta));
+    for (int j = 0; j < C.num_routed; j++) o_sig.push_back(eval_at(C.const_coeffs[C.num_constants + j], zeta));
+    for (int w = 0; w < C.num_wires; w++) o_wires.push_back(eval_at(W.wire_coeffs[w], zeta));
+    for (int i = 0; i < r; i++) { o_zs.push_back(eval_at(W.zs_coeffs[i], zeta)); o_zs_next.push_back(eval_at(W.zs_coeffs[i], zeta_w)); }
+    for (int i = 0; i < r * C.npp; i++) o_pp.push_back(eval_at(W.zs_coeffs[r + i], zeta));
+    for (int i = 0; i < r * C.qdf; i++) o_quot.push_back(eval_at(W.q_coeffs[i], zeta));
+    if (flags & 4) o_quot[0] = gl::eadd(o_quot[0], gl::eb(12345));
+  } else {
+    for (int g = 0; g < C.ngroups; g++) o_const.push_back(gl::eb(C.sel_fill));
+    for (int g = 0; g < C.nls; g++) o_const.push_back(gl::e0());
+    for (int g = 0; g < C.num_gate_consts; g++) o_const.push_back(eval_at(C.gate_const_coeffs[g], zeta));
+    for (int j = 0; j < C.num_routed; j++) o_sig.push_back(gl::escale(C.k_is[j], zeta));
+    for (int w = 0; w < C.num_wires; w++) o_wires.push_back(eval_at(W.wire_coeffs[w], zeta));
+    for (int i = 0; i < r; i++) { o_zs.push_back(gl::eb(1)); o_zs_next.push_back(gl::eb(1)); }
+    for (int i = 0; i < r * C.npp; i++) o_pp.push_back(gl::eb(1));
+    for (int i = 0; i < r * C.qdf; i++) o_quot.push_back(gl::e0());
+    if (flags & 4) o_quot[0] = gl::eb(12345);
+  }
   for (int k = 0; k < r * C.nlp; k++) { o_lzs.push_back(eval_at(W.lzs_coeffs[k], zeta)); o_lzs_next.push_back(eval_at(W.lzs_coeffs[k], zeta_w)); }
   std::vector<E> b1, b2;
   for (auto* v : {&o_const, &o_sig, &o_wires, &o_zs, &o_pp, &o_quot, &o_lzs}) b1.insert(b1.end(), v->begin(), v->end());
@@ -601,10 +997,17 @@ char* dupstr(const std::string& s) { char* p = (char*)malloc(s.size() + 1); memc
 extern "C" {
 
 // spec: degree_bits, num_public_inputs, lookups (0 none, 1/2/3 table sets, see below), circuit_seed
-void* p2v_gen_circuit_new(int degree_bits, int num_pis, int lookups, uint64_t circuit_seed, int num_queries, int pow_bits) {
+// mode 0: the degenerate circuit (gate filters 0 at every point), `ngroups` selector groups
+//         (1: the column is NoopGate's index); mode 1: a real circuit over the recursion gate
+//         set; mode 2: a real circuit over a small gate set (Noop, Constant, PublicInput,
+//         Arithmetic) that fits one selector group.  Real modes choose their own groups.
+void* p2v_gen_circuit_new2(int degree_bits, int num_pis, int lookups, uint64_t circuit_seed, int num_queries, int pow_bits,
+                           int ngroups, int mode) {
   try {
     auto* C = new Circuit();
     C->degree_bits = degree_bits; C->num_pis = num_pis; C->circuit_seed = circuit_seed;
+    if (ngroups > 0) C->ngroups = ngroups;
+    C->real = mode != 0; C->gate_set = mode == 2 ? 1 : 0;
     if (num_queries > 0) C->num_queries = num_queries;
     if (pow_bits >= 0) C->pow_bits = pow_bits;
     if (lookups) {
@@ -621,11 +1024,37 @@ void* p2v_gen_circuit_new(int degree_bits, int num_pis, int lookups, uint64_t ci
     return C;
   } catch (std::exception& e) { g_err = e.what(); return nullptr; }
 }
+void* p2v_gen_circuit_new(int degree_bits, int num_pis, int lookups, uint64_t circuit_seed, int num_queries, int pow_bits) {
+  return p2v_gen_circuit_new2(degree_bits, num_pis, lookups, circuit_seed, num_queries, pow_bits, 0, 0);
+}
 void p2v_gen_circuit_free(void* c) { delete (Circuit*)c; }
+// A witness row of gate `gate` of a real-mode circuit (plonky2 semantics, gates.hpp fill()) with
+// random free inputs and row constants: wires (num_wires), consts (num_gate_consts), pih (4).
+// Returns the number of constraints of the gate's program (all zero on this row), < 0 on error.
+int p2v_gen_gate_row(void* c, int gate, uint64_t seed, uint64_t* wires, uint64_t* consts, uint64_t* pih) {
+  try {
+    const Circuit& C = *(Circuit*)c;
+    if (!C.real || gate < 0 || gate >= (int)C.G.size()) { g_err = "p2v_gen_gate_row: not a real-mode gate"; return -1; }
+    gg::Rng rg(seed);
+    const int NW = C.num_wires, NK = C.num_gate_consts;
+    for (int i = 0; i < 4; i++) pih[i] = rg.field();
+    for (int i = 0; i < NK; i++) consts[i] = i < gg::num_row_constants(C.G[gate]) ? rg.field() : 0;
+    std::vector<uint8_t> pre(NW, 0);
+    gg::fill(C.G[gate], wires, pre.data(), NW, consts, pih, rg);
+    std::vector<u64> out;
+    gg::eval(C.G[gate], wires, NW, consts, NK, pih, out);
+    for (u64 x : out) if (x) { g_err = "p2v_gen_gate_row: row does not satisfy the gate"; return -2; }
+    return (int)out.size();
+  } catch (std::exception& e) { g_err = e.what(); return -3; }
+}
+int p2v_gen_num_gates(void* c) { return (int)((Circuit*)c)->gates.size(); }
 const char* p2v_gen_common_json(void* c) { return ((Circuit*)c)->common_json.c_str(); }
 const char* p2v_gen_vkey_json(void* c) { return ((Circuit*)c)->vkey_json.c_str(); }
 void* p2v_gen_witness_new(void* c, uint64_t seed) {
-  try { return make_witness(*(Circuit*)c, seed); } catch (std::exception& e) { g_err = e.what(); return nullptr; }
+  try {
+    const Circuit& C = *(Circuit*)c;
+    return C.real ? make_witness_real(C, seed) : make_witness(C, seed);
+  } catch (std::exception& e) { g_err = e.what(); return nullptr; }
 }
 void p2v_gen_witness_free(void* w) { delete (Witness*)w; }
 char* p2v_gen_proof_json(void* c, void* w, uint64_t pi_seed) {

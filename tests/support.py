@@ -115,6 +115,9 @@ class Generator:
         vp = ctypes.c_void_p
         L.p2v_gen_circuit_new.restype = vp
         L.p2v_gen_circuit_new.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+        L.p2v_gen_circuit_new2.restype = vp
+        L.p2v_gen_circuit_new2.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int]
         L.p2v_gen_common_json.restype = ctypes.c_char_p
         L.p2v_gen_common_json.argtypes = [vp]
         L.p2v_gen_vkey_json.restype = ctypes.c_char_p
@@ -128,11 +131,16 @@ class Generator:
         L.p2v_gen_proof_json_flags.restype = vp
         L.p2v_gen_proof_json_flags.argtypes = [vp, vp, ctypes.c_uint64, ctypes.c_uint]
         L.p2v_gen_free_str.argtypes = [vp]
+        L.p2v_gen_gate_row.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, vp, vp, vp]
+        L.p2v_gen_num_gates.argtypes = [vp]
         L.p2v_gen_last_error.restype = ctypes.c_char_p
         self.L = L
 
-    def circuit(self, degree_bits=12, num_pis=4, lookups=0, seed=1, queries=28, pow_bits=16):
-        h = self.L.p2v_gen_circuit_new(degree_bits, num_pis, lookups, seed, queries, pow_bits)
+    def circuit(self, degree_bits=12, num_pis=4, lookups=0, seed=1, queries=28, pow_bits=16, ngroups=0, mode=0):
+        """mode 0: degenerate circuit (every gate filter 0), `ngroups` selector groups (0: 3);
+        mode 1: real circuit over the recursion gate set; mode 2: real circuit, small gate set
+        in one selector group."""
+        h = self.L.p2v_gen_circuit_new2(degree_bits, num_pis, lookups, seed, queries, pow_bits, ngroups, mode)
         if not h:
             raise RuntimeError(self.L.p2v_gen_last_error().decode())
         return GenCircuit(self, h)
@@ -153,6 +161,16 @@ class GenCircuit:
             self._wit[seed] = w
         return self._wit[seed]
 
+    def gate_row(self, gate: int, seed: int, num_wires=135, num_consts=2):
+        """(wires, consts, pih) of a witness row that satisfies gate `gate` (real modes)."""
+        w = np.zeros(num_wires, np.uint64)
+        k = np.zeros(num_consts, np.uint64)
+        h = np.zeros(4, np.uint64)
+        n = self.g.L.p2v_gen_gate_row(self.h, gate, seed, w.ctypes.data, k.ctypes.data, h.ctypes.data)
+        if n < 0:
+            raise RuntimeError(self.g.L.p2v_gen_last_error().decode())
+        return w, k, h, n
+
     def proof(self, wseed=1, pseed=1, flags=0) -> bytes:
         w = self.witness(wseed)
         ptr = self.g.L.p2v_gen_proof_json_flags(self.h, w, pseed, flags)
@@ -168,9 +186,9 @@ def generator() -> Generator:
     return Generator()
 
 
-@lru_cache(maxsize=8)
-def gen_circuit(degree_bits=6, num_pis=4, lookups=0, seed=1, queries=28, pow_bits=16) -> GenCircuit:
-    return generator().circuit(degree_bits, num_pis, lookups, seed, queries, pow_bits)
+@lru_cache(maxsize=16)
+def gen_circuit(degree_bits=6, num_pis=4, lookups=0, seed=1, queries=28, pow_bits=16, ngroups=0, mode=0) -> GenCircuit:
+    return generator().circuit(degree_bits, num_pis, lookups, seed, queries, pow_bits, ngroups, mode)
 
 
 # ----------------------------------------------------------------------------- mutations
@@ -178,6 +196,56 @@ def mutate(proof: bytes, fn) -> bytes:
     d = json.loads(proof)
     fn(d)
     return json.dumps(d, separators=(",", ":")).encode()
+
+
+OPENING_KEYS = ("constants", "plonk_sigmas", "plonk_zs", "plonk_zs_next", "partial_products", "lookup_zs", "lookup_zs_next")
+
+
+def randomize_openings(proof: bytes, seed: int, keys=OPENING_KEYS) -> bytes:
+    """Replace the opened values under `keys` (OpeningSet, Types.hs:265-279) by uniform F^2
+    elements: gate selectors S_g(zeta), lookup selectors, sigmas, Z, partial products and the
+    lookup polynomials then take arbitrary values, so every vanishing term is non-trivial."""
+    import random
+    rnd = random.Random(seed)
+
+    def f(d):
+        o = d["proof"]["openings"]
+        for k in keys:
+            o[k] = [[rnd.randrange(P), rnd.randrange(P)] for _ in o[k]]
+    return mutate(proof, f)
+
+
+def trace_offsets(r: int, S: int, Q: int) -> dict:
+    """Word offsets of the debug trace (include/p2v.h)."""
+    o = {"pi_hash": 0, "betas": 4}
+    o["gammas"] = o["betas"] + r
+    o["alphas"] = o["gammas"] + r
+    o["deltas"] = o["alphas"] + r
+    o["zeta"] = o["deltas"] + 4 * r
+    o["fri_alpha"] = o["zeta"] + 2
+    o["fri_betas"] = o["fri_alpha"] + 2
+    o["pow"] = o["fri_betas"] + 2 * S
+    o["query_idx"] = o["pow"] + 1
+    o["combined"] = o["query_idx"] + Q
+    o["quotient"] = o["combined"] + 2 * r
+    o["q_initial"] = o["quotient"] + 2 * r
+    o["q_folded"] = o["q_initial"] + 2 * Q
+    o["q_final"] = o["q_folded"] + 2 * Q
+    o["flags"] = o["q_final"] + 2 * Q
+    o["lut_re"] = o["flags"] + 1
+    return o
+
+
+def circuit_shape(common: bytes):
+    """(r, S, Q) of a generated circuit's common data (ConstantArityBits strategy)."""
+    c = json.loads(common)
+    fc = c["config"]["fri_config"]
+    a, fb = fc["reduction_strategy"]["ConstantArityBits"]
+    logn, S = c["fri_params"]["degree_bits"], 0
+    while logn > fb:
+        logn -= a
+        S += 1
+    return c["config"]["num_challenges"], S, fc["num_query_rounds"]
 
 
 def p2v_module():

@@ -48,6 +48,73 @@ def test_gpu_matches_oracle_status_and_trace(p2v, nb, lk):
         assert np.array_equal(tr[i], otr), (i, np.nonzero(tr[i] != otr)[0][:10])
 
 
+def _gpu_vs_oracle(p2v, gc, cases, **kw):
+    """Statuses and full traces of `cases` on the GPU equal the oracle's, word for word."""
+    O = oracle()
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    res, tr = p2v.BatchVerifier(vk, 0, len(cases)).run(vk.pack_many(cases), trace=True, **kw)
+    sts, otrs = [], []
+    for i, proof in enumerate(cases):
+        st, otr = O.verify_json(gc.common, gc.vkey, proof, trace=True, **kw)
+        assert res[i] == st, (i, int(res[i]), st)
+        assert np.array_equal(tr[i], otr), (i, np.nonzero(tr[i] != otr)[0][:10])
+        sts.append(st)
+        otrs.append(otr)
+    return sts, np.array(otrs)
+
+
+@pytest.mark.parametrize("mode,nb", [(1, 6), (2, 6), (1, 8), (1, 12)])
+def test_gpu_real_circuits_vs_oracle(p2v, mode, nb):
+    """Real circuits (every gate on rows, selector polynomials, copy constraints with a real
+    sigma, Z / partial products, a genuine quotient): every vanishing term is non-zero at zeta.
+    Valid proofs accept; perturbed wire / sigma / Z / Z(omega zeta) / partial-product /
+    selector openings break the identity; statuses and traces equal the oracle's."""
+    from support import circuit_shape, trace_offsets
+    from test_real_circuits import _real_reject_cases
+    gc = gen_circuit(nb, 4, 0, 1, 28, 16, 0, mode)
+    cases = _real_reject_cases(gc) if nb < 12 else _real_reject_cases(gc)[:5]
+    sts, otrs = _gpu_vs_oracle(p2v, gc, [c[0] for c in cases])
+    assert sts == [c[1] for c in cases]
+    off = trace_offsets(*circuit_shape(gc.common))
+    r = circuit_shape(gc.common)[0]
+    assert (otrs[:, off["combined"]: off["combined"] + 2 * r] != 0).all()
+
+
+RANDOMIZED = {
+    "all": None,   # support.OPENING_KEYS
+    "permutation": ("plonk_sigmas", "plonk_zs", "plonk_zs_next", "partial_products"),
+    "selectors": ("constants",),
+    "lookup": ("constants", "lookup_zs", "lookup_zs_next"),
+}
+
+
+@pytest.mark.parametrize("nb,lk,ng", [(6, 0, 1), (6, 0, 3), (6, 1, 1), (6, 1, 3), (6, 2, 3), (8, 0, 3), (8, 1, 1), (12, 0, 3), (12, 1, 3)])
+def test_gpu_randomized_openings_vs_oracle(p2v, nb, lk, ng):
+    """openings replaced by uniform F^2 values (gate selectors S_g(zeta) and
+    lookup selectors, sigmas, Z, Z(omega zeta), partial products, lookup polynomials), on
+    circuits with one and with several selector groups, with and without lookup tables.  Every
+    Z(1)-boundary, partial-product, selector-weighted gate and lookup term is then a non-zero
+    value; C_i must equal the oracle's bit for bit and may not be 0."""
+    from support import OPENING_KEYS, circuit_shape, randomize_openings, trace_offsets
+    gc = gen_circuit(nb, 4, lk, 1, 28, 16, ng, 0)
+    base = [gc.proof(1, 1), gc.proof(2, 2)]
+    cases = []
+    for v, keys in enumerate(RANDOMIZED.values()):
+        if keys == RANDOMIZED["lookup"] and not lk:
+            continue
+        for b, pr in enumerate(base):
+            cases.append(randomize_openings(pr, 1000 * nb + 100 * lk + 10 * v + b, keys or OPENING_KEYS))
+    sts, otrs = _gpu_vs_oracle(p2v, gc, cases)
+    r, S, Q = circuit_shape(gc.common)
+    off = trace_offsets(r, S, Q)
+    comb = otrs[:, off["combined"]: off["combined"] + 2 * r]
+    assert (comb != 0).all()
+    assert len({tuple(c) for c in comb.tolist()}) == len(cases)
+    assert set(sts) == {0}
+    if lk:   # evalFinalRE of every table in every round, compared with the rest of the trace
+        assert otrs[:, off["lut_re"]:].any(axis=1).all()
+
+
 def test_gpu_golden_fixtures(p2v):
     exp = json.load(open(os.path.join(GOLDEN, "expected.json")))["cases"]
 

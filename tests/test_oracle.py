@@ -67,10 +67,10 @@ def test_gate_parser_grammar(gate, kind):
 def test_generated_proofs_accept_and_perm_count():
     O = oracle()
     for lk in (0, 1):
-        gc = gen_circuit(6, 4, lk)
-        for w, s in ((1, 1), (2, 3)):
-            O.L.or_perm_count_reset()
-            assert O.verify_json(gc.common, gc.vkey, gc.proof(w, s)) == 1
+        for ng in (0, 1):   # 3 selector groups / one group (the column is NoopGate's index)
+            gc = gen_circuit(6, 4, lk, 1, 28, 16, ng)
+            for w, s in ((1, 1), (2, 3)):
+                assert O.verify_json(gc.common, gc.vkey, gc.proof(w, s)) == 1
     # permutation-count model of SURVEY.md §8d at n = 6 (1727) + ceil(#PI/8) for the PI hash
     gc = gen_circuit(6, 4, 0)
     pr = gc.proof(1, 1)
@@ -115,7 +115,8 @@ def _reject_cases(gc):
         (mutate(base, leaf), -1),        # initial-tree Merkle failure (Plonk/FRI.hs:108)
         (mutate(base, sib), -2),         # step Merkle failure (Plonk/FRI.hs:310)
         (mutate(base, powm), 0),         # proof-of-work (Plonk/FRI.hs:212-216)
-        (mutate(base, wire), 0),         # opening changed: Plonk identity fails
+        (mutate(base, wire), 0),         # opening changed: on this degenerate circuit C_i stays 0,
+                                         # the transcript moves and the proof fails by its PoW
         (mutate(gc.proof(1, 5, flags=2), later_leaf_after_final_fail), 0),
     ]
 
@@ -126,6 +127,19 @@ def test_reject_paths_follow_reference_order(lk):
     gc = gen_circuit(6, 4, lk)
     for proof, expect in _reject_cases(gc):
         assert O.verify_json(gc.common, gc.vkey, proof) == expect
+
+
+def test_degenerate_wire_mutation_fails_by_pow_not_identity():
+    """on the degenerate circuit a changed wire opening leaves C_i = 0 (gate filters
+    0, sigma = k X); the proof is rejected by its proof of work.  The real circuits of
+    test_real_circuits.py are the ones where the same mutation breaks the Plonk identity."""
+    from support import circuit_shape, trace_offsets
+    O = oracle()
+    gc = gen_circuit(6, 4, 0)
+    proof = _reject_cases(gc)[6][0]
+    st, tr = O.verify_json(gc.common, gc.vkey, proof, trace=True)
+    fl = int(tr[trace_offsets(*circuit_shape(gc.common))["flags"]])
+    assert st == 0 and fl == 1   # eqs_ok, not pow_ok
 
 
 def test_value_canonicalisation_in_json():
