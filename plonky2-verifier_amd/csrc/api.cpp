@@ -19,6 +19,8 @@ extern "C" __global__ void k_phase1(DevCircuit, int, int);
 extern "C" __global__ void k_merkle(DevCircuit);
 extern "C" __global__ void k_fri(DevCircuit);
 extern "C" __global__ void k_vanish(DevCircuit);
+extern "C" __global__ void k_vanish_poseidon(DevCircuit);
+extern "C" __global__ void k_vanish_coset(DevCircuit);
 extern "C" __global__ void k_lut(DevCircuit);
 extern "C" __global__ void k_vanish_final(DevCircuit);
 extern "C" __global__ void k_status(DevCircuit, int8_t*, uint64_t*, int64_t);
@@ -73,6 +75,8 @@ struct p2v_verifier {
   int transcript_mode = 0;          // 0 auto, 1 row, 2 quad (env P2V_TRANSCRIPT)
   int quad_min_batch = 2048;        // auto: quad form from this batch size on
   bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
+  int side_prio = 1;                // side stream at the device's highest priority (env P2V_SIDE_PRIO=0: default priority)
+  bool debug_sync = false;          // env P2V_DEBUG_SYNC=1: name each launch on stderr and synchronise after it (fault isolation)
   // JSON ingest on the device (p2v_verifier_run_json): the current template and its device
   // form, and buffers grown on demand
   ProofTemplate tmpl;
@@ -211,6 +215,8 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   v->circ = pc; v->device = device; v->max_batch = max_batch;
   v->Bmax = (max_batch + 63) / 64 * 64;
   if (const char* ss = getenv("P2V_SINGLE_STREAM")) v->single_stream = ss[0] == '1';
+  if (const char* sp = getenv("P2V_SIDE_PRIO")) v->side_prio = sp[0] == '1';
+  if (const char* ds = getenv("P2V_DEBUG_SYNC")) v->debug_sync = ds[0] == '1';
   if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : 0;
   DevCircuit& d = v->dc;
   memset(&d, 0, sizeof d);
@@ -318,9 +324,12 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   std::vector<int32_t> vit;
   {
     auto item = [&](int t, int a_, int b_, int64_t first) { vit.push_back(t); vit.push_back(a_); vit.push_back(b_); vit.push_back((int32_t)first); };
+    d.vcls[0] = 0;
     for (int g = 0; g < C.n_gate_eval; g++)
       if (gkind[g] == G_POSEIDON) for (int k = 0; k < P2V_POSEIDON_PARTS; k++) item(VI_GATE, g, k, p2v_poseidon_part_first_term(k));
+    d.vcls[1] = (int)(vit.size() / 4);
     for (int g = 0; g < C.n_gate_eval; g++) if (gkind[g] == G_COSET) item(VI_GATE, g, 0, 0);
+    d.vcls[2] = (int)(vit.size() / 4);
     for (int g = 0; g < C.n_gate_eval; g++) if (gkind[g] != G_POSEIDON && gkind[g] != G_COSET) item(VI_GATE, g, 0, 0);
     for (int j = 0; j < d.r; j++) item(VI_PP, j, 0, d.r + (int64_t)j * d.n_pp_terms);
     if (d.nluts > 0)
@@ -328,6 +337,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
     item(VI_ZS1, 0, 0, 0);
   }
   d.n_vitems = (int)(vit.size() / 4);
+  d.vcls[3] = d.n_vitems;
   hipError_t e = hipSuccess;
 #define UP(buf, vec) if (e == hipSuccess) e = upload(buf, vec)
   UP(v->t_cs, C.cs_cap); UP(v->t_kis, C.k_is); UP(v->t_gkind, gkind); UP(v->t_gpar, gpar); UP(v->t_ggrp, ggrp); UP(v->t_gwoff, gwoff);
@@ -354,7 +364,15 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (e == hipSuccess) { for (auto& x : v->ev) { e = hipEventCreate(&x); if (e != hipSuccess) break; } v->timed = e == hipSuccess; }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_p1, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_side, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&v->side, hipStreamNonBlocking);
+  // the side stream carries few, long-latency waves (vanishing items, FRI queries) that must
+  // get CU slots while k_merkle floods the device: queue it at the highest priority
+  if (e == hipSuccess) {
+    int least = 0, greatest = 0;
+    if (v->side_prio && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+      e = hipStreamCreateWithPriority(&v->side, hipStreamNonBlocking, greatest);
+    else
+      e = hipStreamCreateWithFlags(&v->side, hipStreamNonBlocking);
+  }
   if (e != hipSuccess) { p2v_verifier_free(v); return fail(P2V_E_DEVICE, std::string("device allocation: ") + hipGetErrorString(e)); }
   d.cs_cap = (const uint64_t*)v->t_cs.p; d.k_is = (const uint64_t*)v->t_kis.p; d.gate_kind = (const int32_t*)v->t_gkind.p;
   d.gate_par = (const int64_t*)v->t_gpar.p; d.gate_grp = (const int32_t*)v->t_ggrp.p; d.gate_woff = (const int32_t*)v->t_gwoff.p;
@@ -393,8 +411,12 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   hipStream_t sd = v->single_stream ? st : v->side;
 #define T0(k, s_) do { if (tm) HCK(hipEventRecord(v->ev[2 * (k)], s_)); } while (0)
 #define T1(k, s_) do { if (tm) HCK(hipEventRecord(v->ev[2 * (k) + 1], s_)); } while (0)
+  // fault isolation (P2V_DEBUG_SYNC=1): each launch is named before it runs and waited for
+#define DBG(name, s_) do { if (v->debug_sync) { fprintf(stderr, "p2v: launched %s\n", name); fflush(stderr); \
+    HCK(hipStreamSynchronize(s_)); HCK(hipGetLastError()); fprintf(stderr, "p2v: finished %s\n", name); fflush(stderr); } } while (0)
   T0(0, st);
   k_transpose<<<dim3((unsigned)((words + 63) / 64), NPB), 256, 0, st>>>(src, words, (int)n, (uint64_t*)v->soa.p, d.B);
+  DBG("k_transpose", st);
   T1(0, st);
   // phase 1: transcript waves + leaf-hash waves in one launch (the leaf sponges do not
   // depend on the challenges, so they fill the GPU while the serial transcripts run)
@@ -408,6 +430,7 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   const int leaf_units = d.Q * d.T * NPB;
   T0(1, st);
   k_phase1<<<nt_blocks + (leaf_units + 3) / 4, 256, 0, st>>>(d, nt_blocks, tl);
+  DBG("k_phase1", st);
   T1(1, st);
   // phase 2: Merkle paths on the main stream; FRI queries and the vanishing kernel (few,
   // long-latency waves) on the side stream, concurrently
@@ -417,26 +440,38 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   }
   T0(7, sd);
   if (d.n_lut_pieces > 0) k_lut<<<(d.r * d.n_lut_pieces * NPB + 3) / 4, 256, 0, sd>>>(d);
+  DBG("k_lut", sd);
   T1(7, sd);
+  // the vanishing items in three kernels (register allocation per class), timed together
   T0(4, sd);
-  k_vanish<<<(d.n_vitems * NPB + 3) / 4, 256, 0, sd>>>(d);
+  if (d.vcls[1] > d.vcls[0]) k_vanish_poseidon<<<((d.vcls[1] - d.vcls[0]) * NPB + 3) / 4, 256, 0, sd>>>(d);
+  DBG("k_vanish_poseidon", sd);
+  if (d.vcls[2] > d.vcls[1]) k_vanish_coset<<<((d.vcls[2] - d.vcls[1]) * NPB + 3) / 4, 256, 0, sd>>>(d);
+  DBG("k_vanish_coset", sd);
+  k_vanish<<<((d.vcls[3] - d.vcls[2]) * NPB + 3) / 4, 256, 0, sd>>>(d);
+  DBG("k_vanish", sd);
   T1(4, sd);
   T0(6, sd);
   k_vanish_final<<<(d.B + 255) / 256, 256, 0, sd>>>(d);
+  DBG("k_vanish_final", sd);
   T1(6, sd);
   T0(3, sd);
   k_fri<<<(d.Q * NPB + 3) / 4, 256, 0, sd>>>(d);
+  DBG("k_fri", sd);
   T1(3, sd);
   if (sd != st) HCK(hipEventRecord(v->dep_side, sd));
   T0(2, st);
   k_merkle<<<(leaf_units + 3) / 4, 256, 0, st>>>(d);
+  DBG("k_merkle", st);
   T1(2, st);
   if (sd != st) HCK(hipStreamWaitEvent(st, v->dep_side, 0));
   T0(5, st);
   k_status<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(d, dres, dtrace, C.trace_words);
+  DBG("k_status", st);
   T1(5, st);
 #undef T0
 #undef T1
+#undef DBG
   HCK(hipGetLastError());
   if (!(flags & P2V_FLAG_RESULT_DEVICE)) {
     HCK(hipMemcpyAsync(v->h_res, dres, n, hipMemcpyDeviceToHost, st));

@@ -64,6 +64,7 @@ struct DevCircuit {
   int32_t ntops;
   const int32_t* vitems;           // vanishing work items [n_vitems][4] = {VI_*, a, b, first term}
   int32_t n_vitems;
+  int32_t vcls[4];                 // item ranges of the vanishing kernel classes (Poseidon, coset, rest)
   // batch buffers
   const uint64_t* soa;             // [words][B]
   uint64_t* chal;                  // [CH_WORDS][B]

@@ -147,7 +147,11 @@ __device__ __forceinline__ uint64_t mul_nc_dev_v(uint64_t a, uint64_t b) {
   }
 }
 // the general-purpose multiply (FRI, vanishing, gates): the branch-free one-fix-up form
-__device__ __forceinline__ uint64_t mul_nc_dev(uint64_t a, uint64_t b) { return mul_nc_dev_v<1>(a, b); }
+// (P2V_GENERAL_MUL selects another form for measurement / fault isolation builds)
+#ifndef P2V_GENERAL_MUL
+#define P2V_GENERAL_MUL 1
+#endif
+__device__ __forceinline__ uint64_t mul_nc_dev(uint64_t a, uint64_t b) { return mul_nc_dev_v<P2V_GENERAL_MUL>(a, b); }
 #endif
 
 GL_HD void mul128(uint64_t a, uint64_t b, uint64_t& hi, uint64_t& lo) {

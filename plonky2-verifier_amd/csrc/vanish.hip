@@ -30,6 +30,14 @@ __device__ __forceinline__ EE ee_scale(E s, EE x) { return EE{gl::emul(s, x.re),
 __device__ __forceinline__ EE ee_base(E x) { return EE{x, gl::e0()}; }
 __device__ __forceinline__ E lit(uint64_t x) { return gl::eb(x); }
 
+// compile-time loop: f(integral_constant<int, I>) for I in [B, N).  The PoseidonGate programs
+// index their 12-word states only through these, so every index is a constant and the state
+// stays in registers (a partially unrolled `for` left them in scratch memory).
+template <int B, int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < N) { f(std::integral_constant<int, B>{}); sfor<B + 1, N>(f); }
+}
+
 // running sum_k alpha_i^k t_k for every challenge round i < r (r <= P2V_MAX_R, uniform)
 struct Acc {
   E h[P2V_MAX_R];
@@ -67,73 +75,63 @@ __device__ __forceinline__ E esbox(E x) { E x2 = gl::emul(x, x); E x3 = gl::emul
 //   part 3: partial rounds + round 26 ([41,75))           part 4..6: rounds 27..29
 //   part 7: output ([111,123))
 // Term numbering is the gate's own (Acc starts at alpha^first_term of the part).
+// MDS over F^2: the matrix is base-field, so it acts on the two coordinates separately; each
+// is the hashing MDS (p2::mds: 32-bit-half accumulators, one reduction per row), canonicalised
 __device__ __forceinline__ void mds_e(E st[12]) {
-  E t[12];
-#pragma unroll
-  for (int i = 0; i < 12; i++) {
-    E acc = gl::e0();
-#pragma unroll
-    for (int j = 0; j < 12; j++) acc = gl::eadd(acc, E{gl::mul_small(st[j].a, p2::mds_coeff(i, j)), gl::mul_small(st[j].b, p2::mds_coeff(i, j))});
-    t[i] = acc;
-  }
-#pragma unroll
-  for (int i = 0; i < 12; i++) st[i] = t[i];
+  uint64_t a[12], b[12];
+  sfor<0, 12>([&](auto i) { a[i] = st[i].a; b[i] = st[i].b; });
+  p2::mds(a);
+  p2::mds(b);
+  sfor<0, 12>([&](auto i) { st[i] = E{gl::canon(a[i]), gl::canon(b[i])}; });
 }
 // state after a full round whose S-box inputs are the 12 wires starting at w0
+// (the scheduling barriers keep the 12 independent S-boxes from being interleaved, which
+// would need more than 256 VGPRs and spill; these waves are few and latency-bound anyway)
 __device__ __forceinline__ void state_from_sbox_wires(const Vars& V, int w0, E st[12]) {
-#pragma unroll
-  for (int i = 0; i < 12; i++) st[i] = esbox(V.w(w0 + i));
+  sfor<0, 12>([&](auto i) { st[i] = esbox(V.w(w0 + i)); __builtin_amdgcn_sched_barrier(0); });
   mds_e(st);
 }
 // round r: st += rc(r); constraint st - wires[w0..w0+12)
 __device__ __forceinline__ void round_constraint(const Vars& V, Acc& A, E st[12], int r, int w0) {
-#pragma unroll
-  for (int i = 0; i < 12; i++) A.push(gl::esub(gl::eadd(st[i], lit(p2::c_round_constants[12 * r + i])), V.w(w0 + i)));
+  sfor<0, 12>([&](auto i) { A.push(gl::esub(gl::eadd(st[i], lit(p2::c_round_constants[12 * r + i])), V.w(w0 + i))); });
 }
 
 constexpr int POS_SB1 = 29, POS_SBP = 29 + 36, POS_SBF = 29 + 36 + 22;
 
-__device__ __noinline__ void gate_poseidon(const Vars& V, Acc& A, int part) {
+template <int part>
+__device__ __forceinline__ void gate_poseidon_part(const Vars& V, Acc& A) {
   E st[12];
-  if (part == 0) {
+  if constexpr (part == 0) {
     const E one = gl::eb(1);
     const E swap = V.w(24);
     A.push(gl::emul(swap, gl::esub(swap, one)));
     for (int i = 0; i < 4; i++) A.push(gl::esub(gl::emul(swap, gl::esub(V.w(i + 4), V.w(i))), V.w(25 + i)));
-#pragma unroll
-    for (int i = 0; i < 4; i++) st[i] = gl::eadd(V.w(i), V.w(25 + i));
-#pragma unroll
-    for (int i = 4; i < 8; i++) st[i] = gl::esub(V.w(i), V.w(25 + i - 4));
-#pragma unroll
-    for (int i = 8; i < 12; i++) st[i] = V.w(i);
-#pragma unroll
-    for (int i = 0; i < 12; i++) st[i] = esbox(gl::eadd(st[i], lit(p2::c_round_constants[i])));
+    sfor<0, 4>([&](auto i) { st[i] = gl::eadd(V.w(i), V.w(25 + i)); });
+    sfor<4, 8>([&](auto i) { st[i] = gl::esub(V.w(i), V.w(25 + i - 4)); });
+    sfor<8, 12>([&](auto i) { st[i] = V.w(i); });
+    sfor<0, 12>([&](auto i) { st[i] = esbox(gl::eadd(st[i], lit(p2::c_round_constants[i]))); __builtin_amdgcn_sched_barrier(0); });
     mds_e(st);
     round_constraint(V, A, st, 1, POS_SB1);
     return;
   }
-  if (part <= 2) {   // rounds 2, 3
+  else if constexpr (part <= 2) {   // rounds 2, 3
     const int r = part + 1;
     state_from_sbox_wires(V, POS_SB1 + 12 * (r - 2), st);
     round_constraint(V, A, st, r, POS_SB1 + 12 * (r - 1));
     return;
   }
-  if (part == 3) {   // partial rounds (fast form) + the round-26 constraint
+  else if constexpr (part == 3) {   // partial rounds (fast form) + the round-26 constraint
     state_from_sbox_wires(V, POS_SB1 + 24, st);
-#pragma unroll
-    for (int i = 0; i < 12; i++) st[i] = gl::eadd(st[i], lit(p2::c_fast_first_rc[i]));
+    sfor<0, 12>([&](auto i) { st[i] = gl::eadd(st[i], lit(p2::c_fast_first_rc[i])); });
     // mdsInitPartial: partialMdsMatrixCoeff i j = INITIAL_MATRIX ! (j, i)
     E t[12];
     t[0] = st[0];
-#pragma unroll
-    for (int i = 0; i < 11; i++) {
+    sfor<0, 11>([&](auto i) {
       E acc = gl::e0();
-#pragma unroll
-      for (int j = 0; j < 11; j++) acc = gl::eadd(acc, gl::escale(p2::c_fast_init_matrix[11 * j + i], st[1 + j]));
+      sfor<0, 11>([&](auto j) { acc = gl::eadd(acc, gl::escale(p2::c_fast_init_matrix[11 * j + i], st[1 + j])); });
       t[1 + i] = acc;
-    }
-#pragma unroll
-    for (int i = 0; i < 12; i++) st[i] = t[i];
+    });
+    sfor<0, 12>([&](auto i) { st[i] = t[i]; });
 #pragma unroll 1
     for (int r = 0; r < 22; r++) {
       const E sb = V.w(POS_SBP + r);
@@ -142,27 +140,40 @@ __device__ __noinline__ void gate_poseidon(const Vars& V, Acc& A, int part) {
       if (r < 21) z = gl::eadd(z, lit(p2::c_fast_rc[r]));
       // mdsFastPartial r
       E d = E{gl::mul_small(z.a, p2::mds_coeff(0, 0)), gl::mul_small(z.b, p2::mds_coeff(0, 0))};
-#pragma unroll
-      for (int j = 0; j < 11; j++) d = gl::eadd(d, gl::escale(p2::c_fast_w_hats[11 * r + j], st[1 + j]));
-#pragma unroll
-      for (int j = 0; j < 11; j++) st[1 + j] = gl::eadd(st[1 + j], gl::escale(p2::c_fast_vs[11 * r + j], z));
+      sfor<0, 11>([&](auto j) { d = gl::eadd(d, gl::escale(p2::c_fast_w_hats[11 * r + j], st[1 + j])); });
+      sfor<0, 11>([&](auto j) { st[1 + j] = gl::eadd(st[1 + j], gl::escale(p2::c_fast_vs[11 * r + j], z)); });
       st[0] = d;
     }
     round_constraint(V, A, st, 26, POS_SBF);
     return;
   }
-  if (part <= 6) {   // rounds 27..29
+  else if constexpr (part <= 6) {   // rounds 27..29
     const int r = 26 + part - 3;
     state_from_sbox_wires(V, POS_SBF + 12 * (r - 27), st);
     round_constraint(V, A, st, r, POS_SBF + 12 * (r - 26));
     return;
   }
-  state_from_sbox_wires(V, POS_SBF + 36, st);   // output
-  for (int i = 0; i < 12; i++) A.push(gl::esub(st[i], V.w(i + 12)));
+  else {
+    state_from_sbox_wires(V, POS_SBF + 36, st);   // output
+    sfor<0, 12>([&](auto i) { A.push(gl::esub(st[i], V.w(i + 12))); });
+  }
+}
+// the part is a compile-time constant in each branch, so every part gets its own registers
+__device__ __forceinline__ void gate_poseidon(const Vars& V, Acc& A, int part) {
+  switch (part) {
+    case 0: gate_poseidon_part<0>(V, A); break;
+    case 1: gate_poseidon_part<1>(V, A); break;
+    case 2: gate_poseidon_part<2>(V, A); break;
+    case 3: gate_poseidon_part<3>(V, A); break;
+    case 4: gate_poseidon_part<4>(V, A); break;
+    case 5: gate_poseidon_part<5>(V, A); break;
+    case 6: gate_poseidon_part<6>(V, A); break;
+    default: gate_poseidon_part<7>(V, A); break;
+  }
 }
 
 // CosetInterpolationGate, Gate/Custom/CosetInterp.hs:51-121
-__device__ __noinline__ void gate_coset(const DevCircuit& c, const Vars& V, Acc& A, int bits, int64_t degree, const uint64_t* weights, int nweights) {
+__device__ __forceinline__ void gate_coset(const DevCircuit& c, const Vars& V, Acc& A, int bits, int64_t degree, const uint64_t* weights, int nweights) {
   const int64_t npts = (int64_t)1 << bits;
   const int64_t nint = (npts - 2) / (degree - 1);
   const uint64_t gen = c.root_pow2[32 - bits];
@@ -222,7 +233,7 @@ __device__ __forceinline__ E lookup_eq_fixed(const Vars& V, int64_t in0, int64_t
 // RandomAccessGate, Gate/Custom/RandomAccess.hs:47-88.  lookup_eq is the multilinear
 // interpolation sum_i v_i prod_j (bit_j(i) ? b_j : 1 - b_j); it is evaluated by the same
 // pairwise reduction as the reference (exactly the same field element).
-__device__ __noinline__ void gate_random_access(const Vars& V, Acc& A, int nbits, int64_t copies, int64_t extra) {
+__device__ __forceinline__ void gate_random_access(const Vars& V, Acc& A, int nbits, int64_t copies, int64_t extra) {
   const int64_t veclen = (int64_t)1 << nbits, width = 2 + veclen;
   const int64_t bstart = width * copies + extra;
   const E one = gl::eb(1);
@@ -253,9 +264,17 @@ __device__ __noinline__ void gate_random_access(const Vars& V, Acc& A, int nbits
   for (int64_t j = 0; j < extra; j++) A.push(gl::esub(V.k(j), V.w(copies * width + j)));
 }
 
-__device__ void eval_gate(const DevCircuit& c, const Vars& V, Acc& A, int g, int part) {
-  const int kind = c.gate_kind[g];
+// Gate items are split by kernel class so that each kernel is register-allocated for its
+// own programs (one kernel holding all of them needed 256 VGPRs and still spilled):
+// VK_POSEIDON: PoseidonGate parts; VK_COSET: CosetInterpolationGate; VK_MISC: everything else.
+enum { VK_POSEIDON = 0, VK_COSET = 1, VK_MISC = 2 };
+
+template <int CLS>
+__device__ __forceinline__ void eval_gate(const DevCircuit& c, const Vars& V, Acc& A, int g, int part) {
   const int64_t p0 = c.gate_par[3 * g], p1 = c.gate_par[3 * g + 1], p2 = c.gate_par[3 * g + 2];
+  if constexpr (CLS == VK_POSEIDON) { (void)p0; (void)p1; (void)p2; gate_poseidon(V, A, part); return; }
+  if constexpr (CLS == VK_COSET) { gate_coset(c, V, A, (int)p0, p1, c.weights + c.gate_woff[g], c.gate_woff[g + 1] - c.gate_woff[g]); return; }
+  const int kind = c.gate_kind[g];
   const E one = gl::eb(1);
   switch (kind) {
     case 0:   // ArithmeticGate, Constraints.hs:45-46
@@ -283,7 +302,6 @@ __device__ void eval_gate(const DevCircuit& c, const Vars& V, Acc& A, int g, int
         A.push(pr);
       }
       break; }
-    case 3: gate_coset(c, V, A, (int)p0, p1, c.weights + c.gate_woff[g], c.gate_woff[g + 1] - c.gate_woff[g]); break;
     case 4: for (int64_t i = 0; i < p0; i++) A.push(gl::esub(V.k(i), V.w(i))); break;   // ConstantGate
     case 5: {  // ExponentiationGate, :114-128
       const int64_t n = p0;
@@ -306,7 +324,6 @@ __device__ void eval_gate(const DevCircuit& c, const Vars& V, Acc& A, int g, int
     case 10:   // PublicInputGate, :88-89
       for (int i = 0; i < 4; i++) A.push(gl::esub(V.w(i), gl::eb(chal(c, CH_PI(c) + i, V.p))));
       break;
-    case 11: gate_poseidon(V, A, part); break;
     case 12:   // PoseidonMdsGate, Custom/Poseidon.hs:49-59
       for (int i = 0; i < 12; i++) {
         EE acc = EE{gl::e0(), gl::e0()};
@@ -344,7 +361,7 @@ __device__ __forceinline__ uint64_t pow_u(uint64_t x, uint32_t e) {   // uniform
 }
 
 // Z(1) boundary terms: L0(zeta)(Z_i(zeta) - 1), Vanishing.hs:86-95, Algebra/Poly.hs:14-16
-__device__ void item_zs1(const DevCircuit& c, Acc& T, int p) {
+__device__ __forceinline__ void item_zs1(const DevCircuit& c, Acc& T, int p) {
   const E zeta = chal_e(c, CH_ZETA(c), p), one = gl::eb(1);
   const E zeta_n = epow2n(zeta, c.degree_bits);
   E L0;
@@ -354,7 +371,7 @@ __device__ void item_zs1(const DevCircuit& c, Acc& T, int p) {
 }
 
 // partial-product transitions of challenge round j, Vanishing.hs:97-111
-__device__ void item_pp(const DevCircuit& c, Acc& T, int j, int p) {
+__device__ __forceinline__ void item_pp(const DevCircuit& c, Acc& T, int j, int p) {
   const E zeta = chal_e(c, CH_ZETA(c), p), one = gl::eb(1);
   const uint64_t beta = chal(c, CH_BETA(c) + j, p), gamma = chal(c, CH_GAMMA(c) + j, p);
   const int nnum = c.num_routed < c.num_wires ? c.num_routed : c.num_wires;
@@ -380,7 +397,7 @@ __device__ void item_pp(const DevCircuit& c, Acc& T, int j, int p) {
 // delta^16 over the chunks.  ~8 VALU per table entry instead of ~50.  k_lut evaluates pieces
 // of P2V_LUT_PIECE chunks, P_s = sum_{c in piece s} delta^(16 (c - c0_s)) (Cin_c + B Cout_c),
 // on many waves; item_lookup combines them by Horner in delta^(16 P2V_LUT_PIECE).
-__device__ __noinline__ uint64_t lut_piece(const DevCircuit& c, int k, int c0, int c1, uint64_t dde, uint64_t dB) {
+__device__ __forceinline__ uint64_t lut_piece(const DevCircuit& c, int k, int c0, int c1, uint64_t dde, uint64_t dB) {
   constexpr int M = P2V_LUT_CHUNK;
   uint64_t pw[M];
   pw[0] = 1;
@@ -404,7 +421,7 @@ __device__ __noinline__ uint64_t lut_piece(const DevCircuit& c, int k, int c0, i
   return gl::add(ai, gl::mul(dB, ao));
 }
 
-__device__ void item_lookup(const DevCircuit& c, Acc& T, int j, int p) {
+__device__ __forceinline__ void item_lookup(const DevCircuit& c, Acc& T, int j, int p) {
   const E one = gl::eb(1);
   const int nlp = c.nlp, nsldc = nlp - 1;
   const int nlu = c.num_routed / 2 < c.num_wires / 2 ? c.num_routed / 2 : c.num_wires / 2;
@@ -478,7 +495,8 @@ __device__ void item_lookup(const DevCircuit& c, Acc& T, int j, int p) {
 // One vanishing work item for proof p: a contiguous run of terms of the combined sequence
 // sum_k alpha_i^k t_k (Vanishing.hs:48-137).  Item `it` = {type, a, b, first_term}; its
 // partial sums (one F^2 per challenge round) go to vparts[it][2r][B].
-__device__ void vanish_item(const DevCircuit& c, int it, int p) {
+template <int CLS>
+__device__ __forceinline__ void vanish_item(const DevCircuit& c, int it, int p) {
   const int type = c.vitems[4 * it], a = c.vitems[4 * it + 1], b = c.vitems[4 * it + 2];
   const uint32_t first = (uint32_t)c.vitems[4 * it + 3];
   const int r = c.r;
@@ -490,9 +508,9 @@ __device__ void vanish_item(const DevCircuit& c, int it, int p) {
     T.al[i] = i < r ? chal(c, CH_ALPHA(c) + i, p) : 0;
     T.pw[i] = i < r ? pow_u(T.al[i], first) : 0;
   }
-  if (type == VI_ZS1) item_zs1(c, T, p);
-  else if (type == VI_PP) item_pp(c, T, a, p);
-  else if (type == VI_LOOKUP) item_lookup(c, T, a, p);
+  if (CLS == VK_MISC && type == VI_ZS1) item_zs1(c, T, p);
+  else if (CLS == VK_MISC && type == VI_PP) item_pp(c, T, a, p);
+  else if (CLS == VK_MISC && type == VI_LOOKUP) item_lookup(c, T, a, p);
   else {   // gate a (part b): alpha^G0 * S_g(zeta) * sum_k alpha^k c_gk, Vanishing.hs:113-125
     const int grp = c.gate_grp[a];
     const E x = lde(c, c.o_const + 2 * grp, p);   // S_grp(zeta)
@@ -502,7 +520,7 @@ __device__ void vanish_item(const DevCircuit& c, int it, int p) {
     for (int j = c.grp_start[grp]; j < c.grp_end[grp]; j++) if (j != a) s = gl::emul(s, gl::esub(gl::eb((uint64_t)j), x));
     if (c.unit_filters) s = one;
     Vars V{&c, p};
-    eval_gate(c, V, T, a, b);
+    eval_gate<CLS>(c, V, T, a, b);
 #pragma unroll
     for (int i = 0; i < P2V_MAX_R; i++)
       if (i < r) T.h[i] = gl::escale(pow_u(T.al[i], (uint32_t)c.alpha_base_gates), gl::emul(s, T.h[i]));
@@ -532,18 +550,24 @@ extern "C" __global__ void __launch_bounds__(256) k_lut(DevCircuit c) {
   c.lutpart[(int64_t)jp * c.B + p] = lut_piece(c, k, c0, c1, dde, dB);
 }
 
-// one wave = (item, 64 proofs); items are wave-uniform, heaviest first (host order)
-extern "C" __global__ void __launch_bounds__(256) k_vanish(DevCircuit c) {
+// one wave = (item, 64 proofs); items are wave-uniform, heaviest first (host order); the
+// items of kernel class CLS are c.vcls[CLS] .. c.vcls[CLS + 1]
+template <int CLS>
+__device__ __forceinline__ void vanish_body(const DevCircuit& c) {
   const int lane = threadIdx.x & 63;
   const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int NPB = c.B >> 6;
-  if (unit >= c.n_vitems * NPB) return;
-  const int it = unit / NPB, p = (unit % NPB) * 64 + lane;
+  const int i0 = c.vcls[CLS], ni = c.vcls[CLS + 1] - i0;
+  if (unit >= ni * NPB) return;
+  const int it = i0 + unit / NPB, p = (unit % NPB) * 64 + lane;
   // runs concurrently with k_merkle (VALU-bound, many waves): raise the priority of these
   // few latency-bound waves so they do not end up on the critical path
   __builtin_amdgcn_s_setprio(2);
-  vanish_item(c, it, p);
+  vanish_item<CLS>(c, it, p);
 }
+extern "C" __global__ void __launch_bounds__(256) k_vanish_poseidon(DevCircuit c) { vanish_body<VK_POSEIDON>(c); }
+extern "C" __global__ void __launch_bounds__(256) k_vanish_coset(DevCircuit c) { vanish_body<VK_COSET>(c); }
+extern "C" __global__ void __launch_bounds__(256) k_vanish(DevCircuit c) { vanish_body<VK_MISC>(c); }
 
 // sum of the item partials, then Q(zeta)(zeta^n - 1) == C(zeta), Plonk/Verifier.hs:35-51
 extern "C" __global__ void __launch_bounds__(256) k_vanish_final(DevCircuit c) {
