@@ -35,32 +35,50 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 METRIC = "Plonky2 proofs verified/sec (std config, 28 FRI queries) at 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# integer VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD per 4 cycles
-# at 2.4 GHz (full-rate ops: v_mad_u64_u32, v_add/sub/cndmask; measured, tools/microbench/rates.hip)
-VALU_PEAK_G_WAVE_INSTS = 256 * 4 * 2.4 / 4
+# VALU issue roofline (measured, tools/microbench/valu_rates.hip -> profiles/r02_valu_rates.txt and
+# r02_valu_rates_pmc.json): every instruction of the verifier's integer mix (v_mad_u64_u32, the
+# carry-chain v_add/sub/addc_co_u32, v_cndmask_b32_e64, v_lshl_add_u64, v_mul_hi/lo_u32,
+# v_cmp_*_u64, ...) issues at 4.1 SIMD cycles per wave64 instruction even with 8 waves per SIMD;
+# only VOP1/VOP2 32-bit ops (v_add_u32_e32, v_xor, v_mov) pair up two per 4-cycle quad (2.1
+# cycles each), and the PMC counter SQ_ACTIVE_INST_VALU2 counts exactly those quads.  So a
+# launch's VALU issue cycles are 4 * (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2), against an
+# available 1024 SIMDs x 2.4 GHz (the guide's "2 cycles" is the dual-issue case, which this
+# instruction mix reaches for ~1 % of its instructions).
+VALU_SIMDS = 256 * 4
+VALU_CLOCK_GHZ = 2.4
+VALU_QUAD = 4
 
 
 def valu_roofline(kavg, ms_step, B):
-    """VALU issue utilisation from the latest committed rocprofv3 SQ_INSTS_VALU pass
-    (profiles/<tag>_pmc_valu.json, same 4096-proof batch): per kernel over its serial launch
-    time, and for the whole (pipelined) step.  None when no PMC summary is present."""
+    """VALU issue utilisation from the latest committed rocprofv3 VALU pass
+    (profiles/<tag>_pmc_valu.json, same 4096-proof batch): issue cycles per kernel over its
+    serial launch time, and for the whole (pipelined) step.  None when no PMC summary exists."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_valu.json")))
     if not files:
         return None
     pm = json.load(open(files[-1]))
-    ins = {k: v["SQ_INSTS_VALU"] for k, v in pm.items() if not k.startswith("_") and v.get("SQ_INSTS_VALU")}
+    cyc = {}
+    for k, v in pm.items():
+        if k.startswith("_") or not v.get("SQ_INSTS_VALU"):
+            continue
+        # the three vanishing kernels share one timing slot (k_vanish) in libp2v
+        kk = "k_vanish" if k.startswith("k_vanish") and k != "k_vanish_final" else k
+        cyc[kk] = cyc.get(kk, 0.0) + VALU_QUAD * (v["SQ_INSTS_VALU"] - (v.get("SQ_ACTIVE_INST_VALU2") or 0.0))
     scale = B / 4096.0   # the PMC pass ran 4096-proof batches
+    peak = VALU_SIMDS * VALU_CLOCK_GHZ   # G SIMD-cycles per second
     per = {}
-    for k, n in ins.items():
-        if kavg.get(k) and B == 4096:   # per-kernel shares only at the PMC pass's own batch size
-            per[k] = round(n * scale / (kavg[k] * 1e-3) / 1e9 / VALU_PEAK_G_WAVE_INSTS, 3)
-    tot = sum(ins.values()) * scale
-    return {"unit": "G wave-instr/s", "peak": VALU_PEAK_G_WAVE_INSTS,
+    for k, c in cyc.items():
+        if kavg.get(k) and B == 4096:   # per-kernel fractions only at the PMC pass's own batch size
+            per[k] = round(c * scale / (kavg[k] * 1e-3) / 1e9 / peak, 3)
+    tot = sum(cyc.values()) * scale
+    return {"unit": "G SIMD issue-cycles/s", "peak": peak,
             "step_achieved": round(tot / (ms_step * 1e-3) / 1e9, 1),
-            "step_frac": round(tot / (ms_step * 1e-3) / 1e9 / VALU_PEAK_G_WAVE_INSTS, 3),
+            "step_frac": round(tot / (ms_step * 1e-3) / 1e9 / peak, 3),
             "kernel_frac_serial": per, "source": os.path.relpath(files[-1], ROOT),
-            "note": "SQ_INSTS_VALU per step (all kernels) over the pipelined step time: the binding resource"}
+            "model": "issue cycles = 4 x (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) per launch; peak = 1024 SIMDs x 2.4 GHz; "
+                     "per-instruction costs measured in profiles/r02_valu_rates.txt",
+            "note": "all kernels' VALU issue cycles per step over the pipelined step time: the binding resource"}
 
 
 def log(*a):
@@ -269,9 +287,60 @@ def h2d_rate(bvs, tiled, B, expect, steps=3):
     return out
 
 
+C5_PROOFS = 1 << 20       # BASELINE.json configs[4]: 1M proofs over the node's GPUs
+C5_CHUNK = 131072         # per launch: C5's per-GPU share on 8 GPUs
+
+
+def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, backend, dist, streams, steps=1):
+    """BASELINE.json configs[4] (C5): 1 048 576 std proofs sharded over the ranks (contiguous
+    shards, p2v.shard_bounds), each rank verifying its shard in launches of up to 131 072 proofs
+    (the per-GPU share at 8 GPUs) on two workspaces in flight.  The shard is device-resident:
+    the C2 batch tiled on the device to 131 072 distinct HBM rows, reused by every launch of
+    the shard.  Statuses of every launch are checked.  Time = max over ranks."""
+    import torch
+    s, e = p2v.shard_bounds(C5_PROOFS, world, int(os.environ.get("RANK", "0")))
+    n = e - s
+    rows = min(C5_CHUNK, n)
+    reps = (rows + B - 1) // B
+    big = d_proofs.repeat(reps, 1)[:rows].contiguous()
+    exp = d_expect.repeat(reps)[:rows]
+    bvs = [p2v.BatchVerifier(vk, local, rows) for _ in range(2)]
+    res = [torch.empty(rows, dtype=torch.int8, device=dev) for _ in range(2)]
+    chunks = [min(rows, n - k) for k in range(0, n, rows)]
+
+    def one_pass():
+        for i, c in enumerate(chunks):
+            bvs[i % 2].run_device(big.data_ptr(), c, res[i % 2].data_ptr(), stream=streams[i % 2 % len(streams)].cuda_stream, sync=False)
+    one_pass()   # warm-up
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter()
+    for _ in range(steps):
+        one_pass()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t
+    ok = all(bool((res[i % 2][:c] == exp[:c]).all()) for i, c in enumerate(chunks[-2:]))
+    tmax = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    dt = float(tmax.item())
+    del big, bvs, res
+    torch.cuda.empty_cache()
+    return {"proofs": C5_PROOFS * steps, "value": round(C5_PROOFS * steps / dt, 1), "unit": "proofs/s",
+            "per_gpu": round(C5_PROOFS * steps / dt / world, 1), "seconds": round(dt, 4), "n_gpus": world,
+            "shard_per_gpu": n, "launch_proofs": rows, "verified_all": ok,
+            "note": "BASELINE configs[4]: 1M std proofs sharded over the ranks (no data-path collective), "
+                    "launches of <= 131072 device-resident proofs, two in flight per GPU; time = max over ranks"}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks). Under torchrun it must equal WORLD_SIZE; without torchrun and N > 1 "
+                         "bench.py starts the N ranks itself (torch.distributed.run child process)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096, help="proofs per GPU per step")
@@ -284,10 +353,28 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL; the driver's multi-GPU runs) or gloo (rehearsing N ranks on fewer GPUs)")
-    ap.add_argument("--quick", action="store_true", help="device-resident figure only (no ingest / PCIe / CPU legs)")
+    ap.add_argument("--quick", action="store_true", help="device-resident figure only (no ingest / PCIe / CPU / C5 legs)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 leg (1M proofs sharded over the ranks)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus and args.gpus > 1:
+        # N GPUs requested without a launcher: start the N ranks as a child torch.distributed.run
+        # (before anything touches the GPU; no exec) and exit with its status
+        import socket
+        import subprocess
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+        log("[bench] launching", args.gpus, "ranks:", " ".join(cmd))
+        sys.exit(subprocess.call(cmd))
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        log(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a mislabelled number")
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -360,6 +447,9 @@ def main():
     total = B * args.steps * world
     value = total / dt
     kavg = {k: float(np.mean(v)) for k, v in ktimes.items()}
+    c5 = None
+    if not args.quick and not args.no_c5:
+        c5 = c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, args.dist_backend, dist, streams)
     if rank == 0:
         kb = kernel_bytes_model(info, info.trace_words)
         # dominant kernel: the longest launch on the main stream (k_vanish / k_fri / k_lut run on
@@ -401,6 +491,8 @@ def main():
             "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
             "verified_all": ok,
         }
+        if c5 is not None:
+            out["c5"] = c5
         if world == 1 and not args.quick:
             out["ingest"] = ingest_rate(vk, proofs, threads)
             out["h2d_end_to_end"] = h2d_rate(bvs, tiled, B, expect)

@@ -1,0 +1,232 @@
+-- | Drop-in for 'Plonk.Verifier.verifyProof' (reference src/Plonk/Verifier.hs:56) backed by
+-- libp2v, the MI355X batch verifier (include/p2v.h).
+--
+-- The decoded 'Types' values are marshalled field by field into u64 words (the "word-encoded
+-- Types.hs values" of include/p2v.h) and handed to @p2v_circuit_from_words@ /
+-- @p2v_pack_proof_words@; nothing is re-encoded to JSON ('CommonCircuitData' and
+-- 'ProofWithPublicInputs' have no 'ToJSON' instance, src/Types.hs:71,251).  The word layout is
+-- held against the JSON path bit for bit by tests/test_words.py through p2v.py's mirror of
+-- 'circuitWords' / 'proofWords'.
+--
+-- Not compiled in this repository (the image has no GHC).  To use it, add this file to the
+-- reference's source tree as src/Plonk/VerifierGPU.hs and link with
+-- @-L<repo>/plonky2-verifier_amd -lp2v@ (plus an rpath).  @foreign import ccall safe@ keeps the
+-- GHC runtime running during the GPU call.
+{-# LANGUAGE ForeignFunctionInterface, RecordWildCards #-}
+module Plonk.VerifierGPU
+  ( verifyProof
+  , verifyProofBatch
+  , verifyProofBatchOn
+  , GpuCircuit
+  , loadGpuCircuit
+  , verifyWithCircuit
+  , circuitWords
+  , proofWords
+  ) where
+
+import Control.Monad (when, forM_)
+import Data.Bits ((.&.))
+import Data.Char (ord)
+import Data.Int (Int8, Int32, Int64)
+import Data.Word (Word8, Word64)
+import Foreign
+import Foreign.C.String (CString, peekCString)
+import Foreign.C.Types
+import System.IO.Unsafe (unsafePerformIO)
+
+import Algebra.Goldilocks (F, fromF)
+import Algebra.GoldilocksExt (FExt, Ext(..))
+import Gate.Base (Gate(..), KeccakHash(..))
+import Hash.Digest (Digest(..))
+import Misc.Aux (Log2, fromLog2, Range(..))
+import Types
+
+--------------------------------------------------------------------------------
+-- * C ABI (include/p2v.h)
+
+data P2vCircuit
+
+foreign import ccall safe "p2v_circuit_from_words"
+  c_circuit_from_words :: Ptr Word64 -> CSize -> Ptr (Ptr P2vCircuit) -> IO CInt
+foreign import ccall safe "&p2v_circuit_free"
+  c_circuit_free :: FunPtr (Ptr P2vCircuit -> IO ())
+foreign import ccall safe "p2v_circuit_get_info"
+  c_circuit_get_info :: Ptr P2vCircuit -> Ptr () -> IO CInt
+foreign import ccall safe "p2v_pack_proof_words"
+  c_pack_proof_words :: Ptr P2vCircuit -> Ptr Word64 -> CSize -> Ptr Word64 -> IO CInt
+foreign import ccall safe "p2v_verify_batch"
+  c_verify_batch :: Ptr P2vCircuit -> Ptr Word64 -> CSize -> Ptr Int8 -> CInt -> IO CInt
+foreign import ccall safe "p2v_verify_batch_devices"
+  c_verify_batch_devices :: Ptr P2vCircuit -> Ptr Word64 -> CSize -> Ptr Int8 -> Ptr CInt -> CInt -> CSize -> IO CInt
+foreign import ccall unsafe "p2v_last_error_message"
+  c_last_error :: IO CString
+
+wordsCircuitMagic, wordsProofMagic :: Word64
+wordsCircuitMagic = 0x5032564300000001   -- P2V_WORDS_CIRCUIT_MAGIC
+wordsProofMagic   = 0x5032565000000001   -- P2V_WORDS_PROOF_MAGIC
+
+-- | byte offset of @proof_words@ in @p2v_circuit_info@ (12 int32 fields, then int64)
+infoProofWordsOffset :: Int
+infoProofWordsOffset = 48
+
+--------------------------------------------------------------------------------
+-- * Word encoding of the Types.hs values (layout: include/p2v.h)
+
+int :: Int -> Word64
+int = fromIntegral          -- two's complement
+
+lg :: Log2 -> Word64
+lg = int . fromLog2
+
+bool :: Bool -> Word64
+bool b = if b then 1 else 0
+
+felt :: F -> Word64
+felt = fromF
+
+fext :: FExt -> [Word64]
+fext (MkExt a b) = [felt a, felt b]
+
+list :: (a -> [Word64]) -> [a] -> [Word64]
+list f xs = int (length xs) : concatMap f xs
+
+digest :: Digest -> [Word64]
+digest (MkDigest a b c d) = map felt [a, b, c, d]
+
+cap :: MerkleCap -> [Word64]
+cap (MkMerkleCap ds) = list digest ds
+
+friConfig :: FriConfig -> [Word64]
+friConfig MkFriConfig{..} =
+  [lg fri_rate_bits, lg fri_cap_height, lg fri_proof_of_work_bits] ++ strategy fri_reduction_strategy
+    ++ [int fri_num_query_rounds]
+  where
+    strategy (Fixed xs)              = 0 : list (pure . lg) xs
+    strategy (ConstantArityBits a f) = [1, 2, lg a, lg f]
+    strategy (MinSize mb)            = 2 : maybe [0] (\x -> [1, lg x]) mb
+
+gate :: Gate -> [Word64]
+gate g = case g of
+  ArithmeticGate n              -> [0, int n]
+  ArithmeticExtensionGate n     -> [1, int n]
+  BaseSumGate n b               -> [2, int n, int b]
+  CosetInterpolationGate b d ws -> [3, int b, int d] ++ list (pure . felt) ws
+  ConstantGate n                -> [4, int n]
+  ExponentiationGate n          -> [5, int n]
+  LookupGate n h                -> [6, int n] ++ keccak h
+  LookupTableGate n h r         -> [7, int n] ++ keccak h ++ [int r]
+  MulExtensionGate n            -> [8, int n]
+  NoopGate                      -> [9]
+  PublicInputGate               -> [10]
+  PoseidonGate w                -> [11, int w]
+  PoseidonMdsGate w             -> [12, int w]
+  RandomAccessGate b c e        -> [13, int b, int c, int e]
+  ReducingGate n                -> [14, int n]
+  ReducingExtensionGate n       -> [15, int n]
+  UnknownGate name              -> 16 : list (\c -> [fromIntegral (ord c .&. 0xff)]) name
+  where keccak (MkKeccakHash bs) = list (\b -> [fromIntegral (b :: Word8)]) bs
+
+-- | 'VerifierCircuitData' (src/Types.hs:220-240) as words.
+circuitWords :: VerifierCircuitData -> [Word64]
+circuitWords (MkVerifierCircuitData vonly common) = wordsCircuitMagic : (commonW common ++ vonlyW vonly)
+  where
+    commonW MkCommonCircuitData{..} =
+      configW circuit_config ++ paramsW circuit_fri_params ++ list gate circuit_gates
+        ++ selectorsW circuit_selectors_info
+        ++ [ int circuit_quotient_degree_factor, int circuit_num_gate_constraints
+           , int circuit_num_constants, int circuit_num_public_inputs ]
+        ++ list (pure . felt) circuit_k_is
+        ++ [ int circuit_num_partial_products, int circuit_num_lookup_polys, int circuit_num_lookup_selectors ]
+        ++ list (\(MkLookupTable ps) -> list (\(i, o) -> [i, o]) ps) circuit_luts
+    configW MkCircuitConfig{..} =
+      [ int config_num_wires, int config_num_routed_wires, int config_num_constants
+      , bool config_use_base_arithmetic_gate, lg config_security_bits, int config_num_challenges
+      , bool config_zero_knowledge, bool config_randomize_unused_wires, int config_max_quotient_degree_factor ]
+        ++ friConfig config_fri_config
+    paramsW MkFriParams{..} =
+      friConfig fri_config ++ [bool fri_hiding, lg fri_degree_bits] ++ list (pure . lg) fri_reduction_arity_bits
+    selectorsW MkSelectorsInfo{..} =
+      list (pure . int) selector_indices ++ list (\(MkRange a b) -> [int a, int b]) selector_groups
+        ++ maybe [0] (\v -> 1 : list (pure . int) v) selector_vector
+    vonlyW MkVerifierOnlyCircuitData{..} = cap constants_sigmas_cap ++ digest circuit_digest
+
+-- | 'ProofWithPublicInputs' (src/Types.hs:245-279) as words.
+proofWords :: ProofWithPublicInputs -> [Word64]
+proofWords (MkProofWithPublicInputs MkProof{..} pis) =
+  wordsProofMagic : cap wires_cap ++ cap plonk_zs_partial_products_cap ++ cap quotient_polys_cap
+    ++ openingsW openings ++ friW opening_proof ++ list (pure . felt) pis
+  where
+    openingsW MkOpeningSet{..} = concatMap (list fext)
+      [ opening_constants, opening_plonk_sigmas, opening_wires, opening_plonk_zs, opening_plonk_zs_next
+      , opening_partial_products, opening_quotient_polys, opening_lookup_zs, opening_lookup_zs_next ]
+    friW MkFriProof{..} =
+      list cap fri_commit_phase_merkle_caps ++ list roundW fri_query_round_proofs
+        ++ list fext (coeffs fri_final_poly) ++ [felt fri_pow_witness]
+    roundW MkFriQueryRound{..} =
+      list (\(leaf, MkMerkleProof sib) -> list (pure . felt) leaf ++ list digest sib) (evals_proofs fri_initial_trees_proof)
+        ++ list (\MkFriQueryStep{..} -> list fext fri_evals ++ list digest (siblings fri_merkle_proof)) fri_steps
+
+--------------------------------------------------------------------------------
+-- * Circuits and verification
+
+-- | A circuit decoded and validated once by libp2v (circuit-level @error@s surface here).
+newtype GpuCircuit = GpuCircuit (ForeignPtr P2vCircuit)
+
+throwLast :: String -> IO a
+throwLast what = c_last_error >>= peekCString >>= \m -> error (what ++ ": " ++ m)
+
+loadGpuCircuit :: VerifierCircuitData -> IO GpuCircuit
+loadGpuCircuit vkey = withArrayLen (circuitWords vkey) $ \n ws ->
+  alloca $ \out -> do
+    rc <- c_circuit_from_words ws (fromIntegral n) out
+    when (rc /= 0) $ throwLast "p2v_circuit_from_words"
+    GpuCircuit <$> (peek out >>= newForeignPtr c_circuit_free)
+
+-- | statuses: 1 True, 0 False, < 0 the reference's @error@ class (include/p2v.h)
+statusToBool :: Int8 -> Bool
+statusToBool s = case s of
+  1    -> True
+  0    -> False
+  (-1) -> error "checkInitialTreeProofs: at least one Merkle proof failed"
+  (-2) -> error "folding step Merkle proof does not check out"
+  (-3) -> error "folding step evaluation does not match the opening"
+  (-4) -> error "folding step: reduction strategy incompatibility"
+  k    -> error ("p2v status " ++ show k)
+
+-- | Verify a batch on the given devices (one shard per entry, p2v_verify_batch_devices).
+verifyWithCircuit :: GpuCircuit -> [Int] -> [ProofWithPublicInputs] -> IO [Bool]
+verifyWithCircuit _ _ [] = pure []
+verifyWithCircuit (GpuCircuit fc) devices proofs = withForeignPtr fc $ \c -> do
+  pw <- allocaBytes 128 $ \info -> do
+    rc <- c_circuit_get_info c info
+    when (rc /= 0) $ throwLast "p2v_circuit_get_info"
+    peekByteOff info infoProofWordsOffset :: IO Int64
+  let n = length proofs
+      w = fromIntegral pw
+  allocaArray (n * w) $ \buf -> allocaArray n $ \res -> do
+    forM_ (zip [0 ..] proofs) $ \(i, p) ->
+      withArrayLen (proofWords p) $ \m ws -> do
+        rc <- c_pack_proof_words c ws (fromIntegral m) (buf `advancePtr` (i * w))
+        when (rc /= 0) $ throwLast "p2v_pack_proof_words"
+    rc <- case devices of
+      [d] -> c_verify_batch c buf (fromIntegral n) res (fromIntegral d)
+      ds  -> withArrayLen (map fromIntegral ds) $ \k dp ->
+               c_verify_batch_devices c buf (fromIntegral n) res dp (fromIntegral k) 0
+    when (rc /= 0) $ throwLast "p2v_verify_batch"
+    map statusToBool <$> peekArray n res
+
+-- | 'Plonk.Verifier.verifyProof' over a list, on GPU 0.
+verifyProofBatch :: VerifierCircuitData -> [ProofWithPublicInputs] -> IO [Bool]
+verifyProofBatch vkey = verifyProofBatchOn [0] vkey
+
+-- | The same, sharded over several GPUs of the node.
+verifyProofBatchOn :: [Int] -> VerifierCircuitData -> [ProofWithPublicInputs] -> IO [Bool]
+verifyProofBatchOn devices vkey proofs = do
+  c <- loadGpuCircuit vkey
+  verifyWithCircuit c devices proofs
+
+-- | Same type and meaning as 'Plonk.Verifier.verifyProof' (src/Plonk/Verifier.hs:56): True,
+-- False, or the @error@ the reference raises.
+verifyProof :: VerifierCircuitData -> ProofWithPublicInputs -> Bool
+verifyProof vkey proof = unsafePerformIO $ head <$> verifyProofBatch vkey [proof]
+{-# NOINLINE verifyProof #-}

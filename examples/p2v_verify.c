@@ -3,12 +3,16 @@
  * (no Python): what a non-Python host (the Haskell shim of INTEGRATION.md, a C++ service)
  * does with libp2v.
  *
- *   p2v_verify [--pack-only] [--devices N] common.json vkey.json proof.json [proof.json ...]
+ *   p2v_verify [--pack-only] [--devices N] [--dump FILE] common.json vkey.json proof.json [proof.json ...]
+ *   p2v_verify --words [...] circuit.words proof.words [proof.words ...]
  *
  * Prints one line per proof, "<file> <status>": 1 True, 0 False, < 0 the class of `error`
  * the reference would raise (include/p2v.h).  With --pack-only the proofs are decoded and
  * packed (host only, no GPU) and each line carries the packed word count instead.
  * --devices N shards the batch over devices 0..N-1 (p2v_verify_batch_devices).
+ * --words: the inputs are the word-encoded Types.hs values (little-endian u64 files, the
+ * layout of include/p2v.h that a typed host such as the Haskell shim writes) instead of JSON:
+ * p2v_circuit_from_words + p2v_pack_proof_words.  --dump FILE writes the packed words.
  * Exit: 0 done, 2 usage / IO, 3 circuit rejected, 4 a proof did not decode, 5 device error.
  *
  * Build: gcc -O2 -I include examples/p2v_verify.c -L plonky2-verifier_amd -lp2v \
@@ -35,45 +39,64 @@ static char* read_file(const char* path, size_t* len) {
 }
 
 int main(int argc, char** argv) {
-  int pack_only = 0, ndev = 1, a = 1;
+  int pack_only = 0, ndev = 1, a = 1, wordsin = 0;
+  const char* dump = NULL;
   for (; a < argc && argv[a][0] == '-' && argv[a][1] == '-'; a++) {
     if (!strcmp(argv[a], "--pack-only")) pack_only = 1;
+    else if (!strcmp(argv[a], "--words")) wordsin = 1;
     else if (!strcmp(argv[a], "--devices") && a + 1 < argc) ndev = atoi(argv[++a]);
+    else if (!strcmp(argv[a], "--dump") && a + 1 < argc) dump = argv[++a];
     else { fprintf(stderr, "unknown option %s\n", argv[a]); return 2; }
   }
-  if (argc - a < 3 || ndev < 1) {
-    fprintf(stderr, "usage: %s [--pack-only] [--devices N] common.json vkey.json proof.json...\n", argv[0]);
+  const int nhdr = wordsin ? 1 : 2;   /* circuit.words | common.json vkey.json */
+  if (argc - a < nhdr + 1 || ndev < 1) {
+    fprintf(stderr, "usage: %s [--pack-only] [--devices N] [--dump FILE] common.json vkey.json proof.json...\n"
+                    "       %s --words [...] circuit.words proof.words...\n", argv[0], argv[0]);
     return 2;
   }
-  size_t clen, vlen;
+  size_t clen = 0, vlen = 0;
   char* common = read_file(argv[a], &clen);
-  char* vkey = read_file(argv[a + 1], &vlen);
-  if (!common || !vkey) { fprintf(stderr, "cannot read %s / %s\n", argv[a], argv[a + 1]); return 2; }
+  char* vkey = wordsin ? NULL : read_file(argv[a + 1], &vlen);
+  if (!common || (!wordsin && !vkey)) { fprintf(stderr, "cannot read the circuit files\n"); return 2; }
   p2v_circuit* circ = NULL;
-  if (p2v_circuit_from_json(common, clen, vkey, vlen, &circ) != P2V_OK) {
+  int crc = wordsin ? p2v_circuit_from_words((const uint64_t*)common, clen / 8, &circ)
+                    : p2v_circuit_from_json(common, clen, vkey, vlen, &circ);
+  if (crc != P2V_OK) {
     fprintf(stderr, "circuit: %s\n", p2v_last_error_message());
     return 3;
   }
   p2v_circuit_info info;
   p2v_circuit_get_info(circ, &info);
-  const int n = argc - a - 2;
+  const int n = argc - a - nhdr;
   const char** texts = (const char**)calloc((size_t)n, sizeof(char*));
   size_t* lens = (size_t*)calloc((size_t)n, sizeof(size_t));
   for (int i = 0; i < n; i++) {
-    texts[i] = read_file(argv[a + 2 + i], &lens[i]);
-    if (!texts[i]) { fprintf(stderr, "cannot read %s\n", argv[a + 2 + i]); return 2; }
+    texts[i] = read_file(argv[a + nhdr + i], &lens[i]);
+    if (!texts[i]) { fprintf(stderr, "cannot read %s\n", argv[a + nhdr + i]); return 2; }
   }
   uint64_t* words = (uint64_t*)malloc((size_t)n * (size_t)info.proof_words * sizeof(uint64_t));
   int32_t* codes = (int32_t*)malloc((size_t)n * sizeof(int32_t));
-  if (p2v_pack_proofs_json(circ, texts, lens, (size_t)n, words, codes, 0) != 0) {
+  if (wordsin) {
+    for (int i = 0; i < n; i++) {
+      if (p2v_pack_proof_words(circ, (const uint64_t*)texts[i], lens[i] / 8, words + (size_t)i * (size_t)info.proof_words) != P2V_OK) {
+        fprintf(stderr, "%s: %s\n", argv[a + nhdr + i], p2v_last_error_message());
+        return 4;
+      }
+    }
+  } else if (p2v_pack_proofs_json(circ, texts, lens, (size_t)n, words, codes, 0) != 0) {
     for (int i = 0; i < n; i++)
-      if (codes[i] != P2V_OK) fprintf(stderr, "%s: decode error %d\n", argv[a + 2 + i], codes[i]);
+      if (codes[i] != P2V_OK) fprintf(stderr, "%s: decode error %d\n", argv[a + nhdr + i], codes[i]);
     fprintf(stderr, "%s\n", p2v_last_error_message());
     return 4;
   }
+  if (dump) {
+    FILE* f = fopen(dump, "wb");
+    if (!f || fwrite(words, 8, (size_t)n * (size_t)info.proof_words, f) != (size_t)n * (size_t)info.proof_words) { fprintf(stderr, "cannot write %s\n", dump); return 2; }
+    fclose(f);
+  }
   int rc = 0;
   if (pack_only) {
-    for (int i = 0; i < n; i++) printf("%s %lld\n", argv[a + 2 + i], (long long)info.proof_words);
+    for (int i = 0; i < n; i++) printf("%s %lld\n", argv[a + nhdr + i], (long long)info.proof_words);
   } else {
     int8_t* res = (int8_t*)malloc((size_t)n);
     int* devs = (int*)malloc((size_t)ndev * sizeof(int));
@@ -84,7 +107,7 @@ int main(int argc, char** argv) {
       fprintf(stderr, "verify: %s\n", p2v_last_error_message());
       rc = 5;
     } else {
-      for (int i = 0; i < n; i++) printf("%s %d\n", argv[a + 2 + i], (int)res[i]);
+      for (int i = 0; i < n; i++) printf("%s %d\n", argv[a + nhdr + i], (int)res[i]);
     }
     free(res);
     free(devs);

@@ -97,6 +97,53 @@ int  p2v_pack_proof_json(const p2v_circuit* c, const char* proof_json, size_t le
 int  p2v_pack_proofs_json(const p2v_circuit* c, const char* const* jsons, const size_t* lens, size_t n,
                           uint64_t* dst, int32_t* codes, int threads);
 
+/* ---- word-encoded Types.hs values (typed hosts: the Haskell shim) -----------------
+ * A host that holds decoded Types.hs values (VerifierCircuitData, ProofWithPublicInputs —
+ * neither CommonCircuitData nor ProofWithPublicInputs has a ToJSON instance, Types.hs:71,251)
+ * marshals them into u64 words instead of re-encoding JSON.  Encoding (version 1):
+ *   record          its fields in declaration order
+ *   [a]             length n, then the n items
+ *   Int / Log2      two's complement            Bool   0 / 1
+ *   F               its value (any u64; reduced mod p like aeson's Integer, Goldilocks.hs:98-102)
+ *   FExt            re, im                      Digest  4 x F            MerkleCap  [Digest]
+ *   Maybe a         0 | 1, a                    constructor: tag (declaration order), then fields
+ * VerifierCircuitData words = P2V_WORDS_CIRCUIT_MAGIC, then
+ *   CircuitConfig (Types.hs:73-84): num_wires, num_routed_wires, num_constants,
+ *       use_base_arithmetic_gate, security_bits, num_challenges, zero_knowledge,
+ *       randomize_unused_wires, max_quotient_degree_factor, FriConfig
+ *   FriConfig (:116-122): rate_bits, cap_height, proof_of_work_bits,
+ *       reduction_strategy = tag (0 Fixed, 1 ConstantArityBits, 2 MinSize) + [its Log2 fields]
+ *       (Fixed: the arity list; ConstantArityBits: [arity_bits, final_poly_bits]; MinSize: [] or
+ *       [max]), num_query_rounds
+ *   FriParams (:151-157): FriConfig, hiding, degree_bits, [reduction_arity_bits]
+ *   [Gate] (Gate/Base.hs:27-45): tag 0..16 in constructor order (Arithmetic, ArithmeticExtension,
+ *       BaseSum, CosetInterpolation, Constant, Exponentiation, Lookup, LookupTable, MulExtension,
+ *       Noop, PublicInput, Poseidon, PoseidonMds, RandomAccess, Reducing, ReducingExtension,
+ *       Unknown) then its fields; KeccakHash = [Word8] as [u64]; UnknownGate's String as [byte]
+ *   SelectorsInfo (:90-95): [selector_indices], [groups as (start, end)], Maybe [selector_vector]
+ *   quotient_degree_factor, num_gate_constraints, num_constants, num_public_inputs, [k_is],
+ *   num_partial_products, num_lookup_polys, num_lookup_selectors,
+ *   [LookupTable] (each [(Word64, Word64)] as [inp, out] pairs)
+ *   VerifierOnlyCircuitData (:236-240): constants_sigmas_cap, circuit_digest
+ * ProofWithPublicInputs words = P2V_WORDS_PROOF_MAGIC, then
+ *   Proof (:256-263): wires_cap, plonk_zs_partial_products_cap, quotient_polys_cap,
+ *     OpeningSet (:265-276, field order): 9 x [FExt],
+ *     FriProof (:176-181): [MerkleCap] commit caps, [FriQueryRound] (each: [([F], [Digest])]
+ *       initial trees, [([FExt], [Digest])] steps), final_poly [FExt], pow_witness F
+ *   public_inputs [F]
+ * bindings/haskell/Plonk/VerifierGPU.hs writes exactly this; p2v.py circuit_words / proof_words
+ * derive it from the JSON files (tests: words path == JSON path, bit for bit). */
+#define P2V_WORDS_CIRCUIT_MAGIC 0x5032564300000001ULL   /* "P2VC", version 1 */
+#define P2V_WORDS_PROOF_MAGIC   0x5032565000000001ULL   /* "P2VP", version 1 */
+
+/* VerifierCircuitData from its word encoding (same validation and errors as
+ * p2v_circuit_from_json).  Replaces: MkVerifierCircuitData of decoded values (Types.hs:220-224). */
+int  p2v_circuit_from_words(const uint64_t* words, size_t n, p2v_circuit** out);
+/* ProofWithPublicInputs from its word encoding into the circuit's packed layout (dst holds
+ * info.proof_words u64); P2V_E_PARSE on a malformed encoding, P2V_E_SHAPE on list lengths the
+ * circuit does not imply (as p2v_pack_proof_json). */
+int  p2v_pack_proof_words(const p2v_circuit* c, const uint64_t* words, size_t n, uint64_t* dst);
+
 /* ---- verification (GPU) ------------------------------------------------------------ */
 #define P2V_FLAG_INPUT_DEVICE  1u  /* `proofs` is a device pointer on the verifier's device  */
 #define P2V_FLAG_RESULT_DEVICE 2u  /* `results` (and trace) are device pointers              */

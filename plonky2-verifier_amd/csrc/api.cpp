@@ -12,6 +12,9 @@
 #include "../../include/p2v.h"
 #include "circuit.hpp"
 #include "dev.h"
+#ifndef P2V_PROOF_MAJOR
+#define P2V_PROOF_MAJOR 0
+#endif
 #include "gl.h"
 
 extern "C" __global__ void k_transpose(const uint64_t*, int64_t, int, uint64_t*, int);
@@ -105,6 +108,28 @@ int p2v_circuit_from_json(const char* common_json, size_t common_len, const char
     return P2V_OK;
   } catch (const ParseError& e) { return fail(P2V_E_PARSE, e.what()); }
   catch (const CircuitError& e) { return fail(P2V_E_CIRCUIT, e.what()); }
+  catch (const std::exception& e) { return fail(P2V_E_PARSE, e.what()); }
+}
+
+int p2v_circuit_from_words(const uint64_t* words, size_t n, p2v_circuit** out) {
+  if (!words || !out) return fail(P2V_E_ARG, "null argument");
+  try {
+    auto* pc = new p2v_circuit();
+    try { pc->c = parse_circuit_words(words, n); } catch (...) { delete pc; throw; }
+    *out = pc;
+    return P2V_OK;
+  } catch (const ParseError& e) { return fail(P2V_E_PARSE, e.what()); }
+  catch (const CircuitError& e) { return fail(P2V_E_CIRCUIT, e.what()); }
+  catch (const std::exception& e) { return fail(P2V_E_PARSE, e.what()); }
+}
+
+int p2v_pack_proof_words(const p2v_circuit* pc, const uint64_t* words, size_t n, uint64_t* dst) {
+  if (!pc || !words || !dst) return fail(P2V_E_ARG, "null argument");
+  try {
+    pack_proof_words(pc->c, words, n, dst);
+    return P2V_OK;
+  } catch (const ShapeError& e) { return fail(P2V_E_SHAPE, e.what()); }
+  catch (const ParseError& e) { return fail(P2V_E_PARSE, e.what()); }
   catch (const std::exception& e) { return fail(P2V_E_PARSE, e.what()); }
 }
 
@@ -415,8 +440,12 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
 #define DBG(name, s_) do { if (v->debug_sync) { fprintf(stderr, "p2v: launched %s\n", name); fflush(stderr); \
     HCK(hipStreamSynchronize(s_)); HCK(hipGetLastError()); fprintf(stderr, "p2v: finished %s\n", name); fflush(stderr); } } while (0)
   T0(0, st);
+#if P2V_PROOF_MAJOR
+  d.soa = src;   // kernels read the proof-major batch in place (devcommon.h ld())
+#else
   k_transpose<<<dim3((unsigned)((words + 63) / 64), NPB), 256, 0, st>>>(src, words, (int)n, (uint64_t*)v->soa.p, d.B);
   DBG("k_transpose", st);
+#endif
   T1(0, st);
   // phase 1: transcript waves + leaf-hash waves in one launch (the leaf sponges do not
   // depend on the challenges, so they fill the GPU while the serial transcripts run)

@@ -1,5 +1,7 @@
 // circuit.cpp — VerifierCircuitData decode/validation, packed layout, proof packing.
 #include "circuit.hpp"
+#include "gl.h"
+#include "../../include/p2v.h"
 #include <algorithm>
 #include <cstring>
 
@@ -120,6 +122,25 @@ static void digest_of(const JVal& d, uint64_t* out) {   // Hash/Digest.hs:40-44
   for (int i = 0; i < 4; i++) out[i] = j_field(e[i]);
 }
 
+// expandReductionStrategy starts from degree_bits (Plonk/FRI.hs:337-354, :378)
+enum { STRAT_FIXED = 0, STRAT_CONSTANT_ARITY_BITS = 1, STRAT_MIN_SIZE = 2 };   // FriReductionStrategy, Types.hs:128-131
+static void expand_strategy(Circuit& C, int tag, const std::vector<int64_t>& a) {
+  if (tag == STRAT_CONSTANT_ARITY_BITS) {
+    if (a.size() != 2) throw ParseError("ConstantArityBits: expecting [arity_bits, final_poly_bits]");
+    const int ab = (int)a[0], f = (int)a[1];
+    if (ab <= 0 && C.degree_bits > f) throw CircuitError("reduction strategy does not terminate (arity_bits <= 0)");
+    for (int logn = C.degree_bits; logn > f; logn -= ab) C.arities.push_back(ab);
+  } else if (tag == STRAT_FIXED) {
+    for (int64_t x : a) C.arities.push_back((int)x);
+  } else if (tag == STRAT_MIN_SIZE) {
+    throw CircuitError("reduction strategy not implemented (MinSize), Plonk/FRI.hs:342");
+  } else {
+    throw ParseError("FriReductionStrategy: unknown constructor tag");
+  }
+}
+
+static void finalize_circuit(Circuit& C);
+
 Circuit parse_circuit(const JVal& common, const JVal& vkey) {
   Circuit C;
   const JVal& cfg = common.at("config");
@@ -145,17 +166,16 @@ Circuit parse_circuit(const JVal& common, const JVal& vkey) {
   (void)fp.at("reduction_arity_bits").arr();
   (void)fp.at("config");
   C.lde_bits = C.degree_bits + C.rate_bits;
-  // expandReductionStrategy starts from degree_bits (Plonk/FRI.hs:337-354, :378)
   if (rs.keys[0] == "ConstantArityBits") {
     const auto& ab = rs.items[0].arr();
     if (ab.size() != 2) throw ParseError("ConstantArityBits: expecting [arity_bits, final_poly_bits]");
-    int a = (int)j_int(ab[0]), f = (int)j_int(ab[1]);
-    if (a <= 0 && C.degree_bits > f) throw CircuitError("reduction strategy does not terminate (arity_bits <= 0)");
-    for (int logn = C.degree_bits; logn > f; logn -= a) C.arities.push_back(a);
+    expand_strategy(C, STRAT_CONSTANT_ARITY_BITS, {j_int(ab[0]), j_int(ab[1])});
   } else if (rs.keys[0] == "Fixed") {
-    for (const auto& x : rs.items[0].arr()) C.arities.push_back((int)j_int(x));
+    std::vector<int64_t> xs;
+    for (const auto& x : rs.items[0].arr()) xs.push_back(j_int(x));
+    expand_strategy(C, STRAT_FIXED, xs);
   } else if (rs.keys[0] == "MinSize") {
-    throw CircuitError("reduction strategy not implemented (MinSize), Plonk/FRI.hs:342");
+    expand_strategy(C, STRAT_MIN_SIZE, {});
   } else {
     throw ParseError("FromJSON/FriReductionStrategy: unrecognized FRI reduction strategy");
   }
@@ -185,7 +205,13 @@ Circuit parse_circuit(const JVal& common, const JVal& vkey) {
   }
   for (const auto& d : vkey.at("constants_sigmas_cap").arr()) { uint64_t e[4]; digest_of(d, e); C.cs_cap.insert(C.cs_cap.end(), e, e + 4); }
   digest_of(vkey.at("circuit_digest"), C.digest);
+  finalize_circuit(C);
+  return C;
+}
 
+// Validation (circuit-level `error`s) and everything derived from the decoded fields; shared by
+// the JSON and the word-encoded entry points.
+static void finalize_circuit(Circuit& C) {
   // ---------------------------------------------------------------- validation
   // Circuit-level `error`s that the reference raises on every verification of this circuit.
   const int ngroups = (int)C.grp_start.size();
@@ -285,7 +311,6 @@ Circuit parse_circuit(const JVal& common, const JVal& vkey) {
   L.words = w;
   const int S = (int)C.arities.size(), Q = C.num_queries, r = C.r;
   C.trace_words = 4 + 3 * r + 4 * r + 4 + 2 * S + 1 + Q + 4 * r + 6 * Q + 1 + r * (int64_t)C.lut_in.size();
-  return C;
 }
 
 // ------------------------------------------------------------------ packing
@@ -366,6 +391,186 @@ void pack_proof(const Circuit& C, const JVal& root, uint64_t* dst, int32_t* rec)
       P.digests(st[s].at("merkle_proof").at("siblings"), base + L.step_path[s], C.step_depth[s], "step siblings");
     }
   }
+}
+
+// ------------------------------------------------------------------ word-encoded values
+// The Types.hs values themselves, marshalled field by field into u64 words by a typed host
+// (the Haskell shim bindings/haskell/Plonk/VerifierGPU.hs; p2v.py's circuit_words /
+// proof_words mirror it): records in declaration order, lists as [length, items...], Int as
+// two's complement, Bool as 0/1, F as its value (reduced mod p here, as aeson's Integer is),
+// constructors as [tag, fields...] in declaration order.  Layout: include/p2v.h.
+namespace {
+struct WordReader {
+  const uint64_t* w; size_t n; size_t i = 0;
+  uint64_t u(const char* what) { if (i >= n) throw ParseError(std::string("words: truncated at ") + what); return w[i++]; }
+  int64_t s(const char* what) { return (int64_t)u(what); }
+  int64_t len(const char* what) {
+    const int64_t k = s(what);
+    if (k < 0 || (uint64_t)k > n - i) throw ParseError(std::string("words: bad list length of ") + what);
+    return k;
+  }
+  uint64_t f(const char* what) { return u(what) % gl::P; }
+  bool b(const char* what) { const uint64_t x = u(what); if (x > 1) throw ParseError(std::string("words: bad Bool in ") + what); return x == 1; }
+  void magic(uint64_t m) { if (u("magic") != m) throw ParseError("words: bad magic / version"); }
+};
+
+void read_fri_config(WordReader& R, int& rate, int& cap, int& pow, int& tag, std::vector<int64_t>& args, int& nq) {
+  rate = (int)R.s("fri_rate_bits"); cap = (int)R.s("fri_cap_height"); pow = (int)R.s("fri_proof_of_work_bits");
+  tag = (int)R.s("fri_reduction_strategy");
+  const int64_t k = R.len("reduction strategy fields");
+  args.clear();
+  for (int64_t i = 0; i < k; i++) args.push_back(R.s("reduction strategy field"));
+  nq = (int)R.s("fri_num_query_rounds");
+}
+
+const char* gate_name(int k) {
+  static const char* names[] = {"ArithmeticGate", "ArithmeticExtensionGate", "BaseSumGate", "CosetInterpolationGate", "ConstantGate",
+                                "ExponentiationGate", "LookupGate", "LookupTableGate", "MulExtensionGate", "NoopGate", "PublicInputGate",
+                                "PoseidonGate", "PoseidonMdsGate", "RandomAccessGate", "ReducingGate", "ReducingExtensionGate", "UnknownGate"};
+  return k >= 0 && k <= 16 ? names[k] : "UnknownGate";
+}
+}  // namespace
+
+Circuit parse_circuit_words(const uint64_t* w, size_t n) {
+  WordReader R{w, n};
+  R.magic(P2V_WORDS_CIRCUIT_MAGIC);
+  Circuit C;
+  // CircuitConfig (Types.hs:73-84)
+  C.num_wires = (int)R.s("config_num_wires");
+  C.num_routed = (int)R.s("config_num_routed_wires");
+  C.num_gate_consts = (int)R.s("config_num_constants");
+  (void)R.b("config_use_base_arithmetic_gate");
+  (void)R.s("config_security_bits");
+  C.r = (int)R.s("config_num_challenges");
+  (void)R.b("config_zero_knowledge");
+  (void)R.b("config_randomize_unused_wires");
+  C.max_qdf = (int)R.s("config_max_quotient_degree_factor");
+  int tag = 0, tag2 = 0, d0, d1, d2, d3;
+  std::vector<int64_t> sargs, sargs2;
+  read_fri_config(R, C.rate_bits, C.cap_height, C.pow_bits, tag, sargs, C.num_queries);
+  // FriParams (Types.hs:151-157): its own FriConfig copy, hiding, degree_bits, arity bits
+  read_fri_config(R, d0, d1, d2, tag2, sargs2, d3);
+  (void)R.b("fri_hiding");
+  C.degree_bits = (int)R.s("fri_degree_bits");
+  for (int64_t k = R.len("fri_reduction_arity_bits"); k > 0; k--) (void)R.s("fri_reduction_arity_bits");
+  C.lde_bits = C.degree_bits + C.rate_bits;
+  expand_strategy(C, tag, sargs);
+  // gates (Gate/Base.hs:27-45)
+  for (int64_t k = R.len("circuit_gates"); k > 0; k--) {
+    GateDesc g;
+    const int64_t t = R.s("gate constructor");
+    auto field = [&]() { return R.s("gate field"); };
+    std::string params;
+    switch (t) {
+      case G_ARITH: case G_ARITH_EXT: case G_CONST: case G_EXP: case G_MULEXT: case G_POSEIDON: case G_POSEIDON_MDS:
+      case G_REDUCING: case G_REDUCING_EXT:
+        g.p0 = field(); params = std::to_string(g.p0); break;
+      case G_BASESUM: g.p0 = field(); g.p1 = field(); params = std::to_string(g.p0) + ", " + std::to_string(g.p1); break;
+      case G_COSET: {
+        g.p0 = field(); g.p1 = field();
+        for (int64_t m = R.len("barycentric_weights"); m > 0; m--) g.weights.push_back(R.f("barycentric weight"));
+        params = std::to_string(g.p0) + ", " + std::to_string(g.p1) + ", " + std::to_string(g.weights.size()) + " weights";
+        break; }
+      case G_LOOKUP: case G_LOOKUPTABLE:
+        g.p0 = field();
+        for (int64_t m = R.len("lut_hash"); m > 0; m--) (void)R.u("lut_hash byte");
+        if (t == G_LOOKUPTABLE) g.p2 = field();
+        params = std::to_string(g.p0);
+        break;
+      case G_NOOP: case G_PI: break;
+      case G_RANDACC: g.p0 = field(); g.p1 = field(); g.p2 = field();
+        params = std::to_string(g.p0) + ", " + std::to_string(g.p1) + ", " + std::to_string(g.p2); break;
+      case G_UNKNOWN: {
+        std::string name;
+        for (int64_t m = R.len("UnknownGate name"); m > 0; m--) name.push_back((char)R.u("name byte"));
+        params = name;
+        break; }
+      default: throw ParseError("words: unknown Gate constructor tag " + std::to_string(t));
+    }
+    g.kind = (int32_t)t;
+    g.text = std::string(gate_name((int)t)) + "(" + params + ")";
+    C.gates.push_back(std::move(g));
+  }
+  // SelectorsInfo (Types.hs:90-95)
+  for (int64_t k = R.len("selector_indices"); k > 0; k--) C.sel_idx.push_back((int)R.s("selector index"));
+  for (int64_t k = R.len("selector_groups"); k > 0; k--) { C.grp_start.push_back((int)R.s("range_start")); C.grp_end.push_back((int)R.s("range_end")); }
+  if (R.b("selector_vector present")) for (int64_t k = R.len("selector_vector"); k > 0; k--) (void)R.s("selector_vector");
+  C.qdf = (int)R.s("circuit_quotient_degree_factor");
+  C.num_gate_constraints = (int)R.s("circuit_num_gate_constraints");
+  C.num_constants = (int)R.s("circuit_num_constants");
+  C.num_pis = (int)R.s("circuit_num_public_inputs");
+  for (int64_t k = R.len("circuit_k_is"); k > 0; k--) C.k_is.push_back(R.f("k_i"));
+  C.npp = (int)R.s("circuit_num_partial_products");
+  C.nlp = (int)R.s("circuit_num_lookup_polys");
+  C.nls = (int)R.s("circuit_num_lookup_selectors");
+  for (int64_t k = R.len("circuit_luts"); k > 0; k--) {   // LookupTable = [(Word64, Word64)], Types.hs:28-33
+    std::vector<uint64_t> in, out;
+    for (int64_t m = R.len("lookup table"); m > 0; m--) { in.push_back(R.u("lut input") % gl::P); out.push_back(R.u("lut output") % gl::P); }
+    C.lut_in.push_back(std::move(in)); C.lut_out.push_back(std::move(out));
+  }
+  // VerifierOnlyCircuitData (Types.hs:236-240)
+  for (int64_t k = R.len("constants_sigmas_cap"); k > 0; k--) for (int j = 0; j < 4; j++) C.cs_cap.push_back(R.f("cap digest"));
+  for (int j = 0; j < 4; j++) C.digest[j] = R.f("circuit_digest");
+  if (R.i != n) throw ParseError("words: trailing words after VerifierCircuitData");
+  finalize_circuit(C);
+  return C;
+}
+
+void pack_proof_words(const Circuit& C, const uint64_t* w, size_t n, uint64_t* dst) {
+  WordReader R{w, n};
+  R.magic(P2V_WORDS_PROOF_MAGIC);
+  const Layout& L = C.L;
+  auto fields = [&](int64_t off, int64_t want, const char* what) {
+    const int64_t k = R.len(what);
+    if (k != want) throw ShapeError(std::string(what) + ": expected " + std::to_string(want) + " elements, got " + std::to_string(k));
+    for (int64_t i = 0; i < k; i++) dst[off + i] = R.f(what);
+  };
+  auto exts = [&](int64_t off, int64_t want, const char* what) {
+    const int64_t k = R.len(what);
+    if (k != want) throw ShapeError(std::string(what) + ": expected " + std::to_string(want) + " F^2 values, got " + std::to_string(k));
+    for (int64_t i = 0; i < 2 * k; i++) dst[off + i] = R.f(what);
+  };
+  auto digests = [&](int64_t off, int64_t want, const char* what) {
+    const int64_t k = R.len(what);
+    if (k != want) throw ShapeError(std::string(what) + ": expected " + std::to_string(want) + " digests, got " + std::to_string(k));
+    for (int64_t i = 0; i < 4 * k; i++) dst[off + i] = R.f(what);
+  };
+  // Proof (Types.hs:256-263)
+  digests(L.wcap, C.cap_len, "wires_cap");
+  digests(L.zcap, C.cap_len, "plonk_zs_partial_products_cap");
+  digests(L.qcap, C.cap_len, "quotient_polys_cap");
+  // OpeningSet, field order (Types.hs:265-276)
+  exts(L.o_const, C.num_constants, "openings.constants");
+  exts(L.o_sig, C.num_routed, "openings.plonk_sigmas");
+  exts(L.o_wires, C.num_wires, "openings.wires");
+  exts(L.o_zs, C.r, "openings.plonk_zs");
+  exts(L.o_zs_next, C.r, "openings.plonk_zs_next");
+  exts(L.o_pp, (int64_t)C.r * C.npp, "openings.partial_products");
+  exts(L.o_quot, (int64_t)C.r * C.qdf, "openings.quotient_polys");
+  exts(L.o_lzs, (int64_t)C.r * C.nlp, "openings.lookup_zs");
+  exts(L.o_lzs_next, (int64_t)C.r * C.nlp, "openings.lookup_zs_next");
+  // FriProof (Types.hs:176-181)
+  const int S = (int)C.arities.size();
+  if (R.len("commit_phase_merkle_caps") != S) throw ShapeError("commit_phase_merkle_caps: expected " + std::to_string(S));
+  for (int s = 0; s < S; s++) digests(L.ccaps + (int64_t)s * 4 * C.cap_len, C.cap_len, "commit_phase_merkle_caps[s]");
+  if (R.len("query_round_proofs") != C.num_queries) throw ShapeError("query_round_proofs: expected " + std::to_string(C.num_queries));
+  for (int q = 0; q < C.num_queries; q++) {
+    const int64_t base = L.q0 + (int64_t)q * L.qstride;
+    if (R.len("evals_proofs") != 4) throw ShapeError("checkInitialTreeProofs: expecting 4 Merkle proofs for the 4 oracles");
+    for (int t = 0; t < 4; t++) {
+      fields(base + L.leaf[t], C.oracle_width[t], "initial tree leaf");
+      digests(base + L.path[t], C.depth0, "initial tree siblings");
+    }
+    if (R.len("steps") != S) throw ShapeError("steps: expected " + std::to_string(S));
+    for (int s = 0; s < S; s++) {
+      exts(base + L.step_evals[s], 1 << C.arities[s], "step evals");
+      digests(base + L.step_path[s], C.step_depth[s], "step siblings");
+    }
+  }
+  exts(L.final_poly, C.final_len, "final_poly.coeffs");
+  dst[L.pow] = R.f("pow_witness");
+  fields(L.pis, C.num_pis, "public_inputs");   // ProofWithPublicInputs: the_proof, public_inputs
+  if (R.i != n) throw ParseError("words: trailing words after ProofWithPublicInputs");
 }
 
 // ------------------------------------------------------------------ template-guided pack

@@ -68,6 +68,9 @@ struct Circuit {
 };
 
 Circuit parse_circuit(const JVal& common, const JVal& vkey);   // throws ParseError / CircuitError
+// the same from the word-encoded Types.hs values (include/p2v.h, "Word-encoded values")
+Circuit parse_circuit_words(const uint64_t* words, size_t n);   // throws ParseError / CircuitError
+void pack_proof_words(const Circuit& c, const uint64_t* words, size_t n, uint64_t* dst);   // ParseError / ShapeError
 // throws ParseError / ShapeError; rec (optional, [words]) receives each packed word's number ordinal
 void pack_proof(const Circuit& c, const JVal& proof, uint64_t* dst, int32_t* rec = nullptr);
 

@@ -8,7 +8,19 @@ namespace p2d {
 
 using gl::E;
 
-__device__ __forceinline__ uint64_t ld(const DevCircuit& c, int64_t w, int p) { return c.soa[w * c.B + p]; }
+// Proof word w of lane p.  P2V_PROOF_MAJOR = 0: the transposed batch [word][B] written by
+// k_transpose (every load a coalesced 512-B row); 1: the caller's proof-major batch [n][words]
+// read in place (no transpose pass; lanes past n re-read the last proof)
+#ifndef P2V_PROOF_MAJOR
+#define P2V_PROOF_MAJOR 0
+#endif
+__device__ __forceinline__ uint64_t ld(const DevCircuit& c, int64_t w, int p) {
+#if P2V_PROOF_MAJOR
+  return c.soa[(int64_t)min(p, c.n - 1) * c.words + w];
+#else
+  return c.soa[w * c.B + p];
+#endif
+}
 __device__ __forceinline__ E lde(const DevCircuit& c, int64_t w, int p) { return E{ld(c, w, p), ld(c, w + 1, p)}; }
 __device__ __forceinline__ uint64_t& chal(const DevCircuit& c, int64_t w, int p) { return c.chal[w * c.B + p]; }
 __device__ __forceinline__ E chal_e(const DevCircuit& c, int64_t w, int p) { return E{c.chal[w * c.B + p], c.chal[(w + 1) * c.B + p]}; }

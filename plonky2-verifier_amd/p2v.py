@@ -107,6 +107,8 @@ def lib() -> ctypes.CDLL:
     L.p2v_circuit_get_info.argtypes = [vp, ctypes.POINTER(_Info)]
     L.p2v_pack_proof_json.argtypes = [vp, ctypes.c_char_p, sz, u64p]
     L.p2v_pack_proofs_json.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz, u64p, vp, ctypes.c_int]
+    L.p2v_circuit_from_words.argtypes = [u64p, sz, ctypes.POINTER(vp)]
+    L.p2v_pack_proof_words.argtypes = [vp, u64p, sz, u64p]
     L.p2v_device_count.argtypes = []
     L.p2v_verifier_create.argtypes = [vp, ctypes.c_int, sz, ctypes.POINTER(vp)]
     L.p2v_verifier_free.argtypes = [vp]
@@ -176,9 +178,26 @@ class VerifierCircuitData:
         _check(lib().p2v_circuit_from_json(c, len(c), v, len(v), ctypes.byref(h)))
         return cls(h.value)
 
+    @classmethod
+    def from_words(cls, words: np.ndarray) -> "VerifierCircuitData":
+        """The word-encoded Types.hs value (include/p2v.h; what the Haskell shim marshals)."""
+        w = np.ascontiguousarray(words, dtype=np.uint64)
+        h = ctypes.c_void_p()
+        _check(lib().p2v_circuit_from_words(w.ctypes.data, w.size, ctypes.byref(h)))
+        return cls(h.value)
+
     @property
     def handle(self) -> ctypes.c_void_p:
         return self._h
+
+    def pack_words(self, words: np.ndarray, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """A word-encoded ProofWithPublicInputs (include/p2v.h) -> packed u64 words."""
+        w = np.ascontiguousarray(words, dtype=np.uint64)
+        if out is None:
+            out = np.empty(self.info.proof_words, dtype=np.uint64)
+        assert out.dtype == np.uint64 and out.size == self.info.proof_words and out.flags.c_contiguous
+        _check(lib().p2v_pack_proof_words(self._h, w.ctypes.data, w.size, out.ctypes.data))
+        return out
 
     def pack(self, proof_json: Union[str, bytes], out: Optional[np.ndarray] = None) -> np.ndarray:
         """ProofWithPublicInputs JSON (Types.hs:245-254) -> packed u64 words of this circuit."""
@@ -387,16 +406,170 @@ def shard_bounds(n: int, world: int, rank: int):
 
 
 def verify_sharded(vkey: VerifierCircuitData, packed: np.ndarray, rank: int, world: int, device: int,
-                   group=None) -> np.ndarray:
+                   group=None, verify_shard=None) -> np.ndarray:
     """Each rank verifies its shard of `packed` on its own GPU; the int8 statuses are then
-    gathered so every rank holds the full result vector (one small all_gather of results,
-    the only cross-rank traffic)."""
-    import torch
-    import torch.distributed as dist
+    gathered so every rank holds the full result vector (one all_gather of the padded int8
+    shards, the only cross-rank traffic; on the RCCL backend the gather runs on the device).
+    verify_shard(rows, start, end) -> int8 statuses replaces the rank's BatchVerifier (tests
+    inject a CPU verifier to run the sharding with gloo and no GPU)."""
     s, e = shard_bounds(packed.shape[0], world, rank)
-    local = BatchVerifier(vkey, device, max(1, e - s)).run(packed[s:e]) if e > s else np.empty(0, np.int8)
+    if verify_shard is None:
+        def verify_shard(rows, start, end):
+            return BatchVerifier(vkey, device, max(1, end - start)).run(rows)
+    local = np.asarray(verify_shard(packed[s:e], s, e), dtype=np.int8) if e > s else np.empty(0, np.int8)
     if world == 1:
         return local
-    parts = [None] * world
-    dist.all_gather_object(parts, local.tolist(), group=group)
-    return np.array([x for p in parts for x in p], dtype=np.int8)
+    import torch
+    import torch.distributed as dist
+    longest = shard_bounds(packed.shape[0], world, 0)[1]   # shard 0 is a longest one
+    dev = torch.device("cuda", device) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    mine = torch.zeros(max(1, longest), dtype=torch.int8, device=dev)
+    mine[: len(local)] = torch.from_numpy(local).to(dev)
+    parts = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(parts, mine, group=group)
+    out = []
+    for r in range(world):
+        rs, re_ = shard_bounds(packed.shape[0], world, r)
+        out.append(parts[r][: re_ - rs].cpu().numpy())
+    return np.concatenate(out).astype(np.int8)
+
+
+# ----------------------------------------------------------------------------- word encoding
+# The typed-host form of the boundary (include/p2v.h "word-encoded Types.hs values"): what the
+# Haskell shim (bindings/haskell/Plonk/VerifierGPU.hs) marshals from decoded values.  These
+# functions derive the same words from the JSON files, following Types.hs field order and the
+# Gate/Parser.hs grammar, so tests can hold the words path against the JSON path.
+P = 0xFFFFFFFF00000001   # Goldilocks modulus (Algebra/Goldilocks.hs)
+WORDS_CIRCUIT_MAGIC = 0x5032564300000001
+WORDS_PROOF_MAGIC = 0x5032565000000001
+_M64 = (1 << 64) - 1
+
+_GATE_RE = [   # (tag, regex) in Gate/Parser.hs order of alternatives; groups = Int fields
+    (0, r"ArithmeticGate \{ num_ops: (\d+) \}$"),
+    (1, r"ArithmeticExtensionGate \{ num_ops: (\d+) \}$"),
+    (2, r"BaseSumGate \{ num_limbs: (\d+) \} \+ Base: (\d+)$"),
+    (3, r"CosetInterpolationGate \{ subgroup_bits: (\d+), degree: (\d+), barycentric_weights: \[([0-9, ]*)\], "
+        r"_phantom: PhantomData<plonky2_field::goldilocks_field::GoldilocksField> \}<D=2>$"),
+    (4, r"ConstantGate \{ num_consts: (\d+) \}"),
+    (5, r"ExponentiationGate \{ num_power_bits: (\d+) \}"),
+    (6, r"LookupGate \{ num_slots: (\d+), lut_hash: \[([0-9, ]*)\] \}"),
+    (7, r"LookupTableGate \{ num_slots: (\d+), lut_hash: \[([0-9, ]*)\], last_lut_row: (\d+) \}"),
+    (8, r"MulExtensionGate \{ num_ops: (\d+) \}"),
+    (9, r"NoopGate"),
+    (10, r"PublicInputGate"),
+    (11, r"PoseidonGate\(PhantomData<plonky2_field::goldilocks_field::GoldilocksField>\)<WIDTH=(\d+)>$"),
+    (12, r"PoseidonMdsGate\(PhantomData<plonky2_field::goldilocks_field::GoldilocksField>\)<WIDTH=(\d+)>$"),
+    (13, r"RandomAccessGate \{ bits: (\d+), num_copies: (\d+), num_extra_constants: (\d+), "
+         r"_phantom: PhantomData<plonky2_field::goldilocks_field::GoldilocksField> \}<D=2>"),
+    (14, r"ReducingGate \{ num_coeffs: (\d+)(?:<D=2>)? \}"),
+    (15, r"ReducingExtensionGate \{ num_coeffs: (\d+)(?:<D=2>)? \}"),
+]
+
+
+def _gate_words(text: str) -> list:
+    """Gate (Gate/Base.hs:27-45) of a Rust Debug string -> [tag, fields...]."""
+    import re
+    for tag, rx in _GATE_RE:
+        m = re.match(rx, text)
+        if not m:
+            continue
+        g = m.groups()
+        if tag == 3:
+            ws = [int(x) % P for x in g[2].replace(" ", "").split(",") if x]
+            return [tag, int(g[0]), int(g[1]), len(ws)] + ws
+        if tag in (6, 7):
+            hb = [int(x) & 0xFF for x in g[1].replace(" ", "").split(",") if x]
+            return [tag, int(g[0]), len(hb)] + hb + ([int(g[2])] if tag == 7 else [])
+        return [tag] + [int(x) for x in g]
+    name = text.encode()
+    return [16, len(name)] + list(name)
+
+
+def _fri_config_words(fc: dict) -> list:
+    rs = fc["reduction_strategy"]
+    (k, v), = rs.items()
+    tag = {"Fixed": 0, "ConstantArityBits": 1, "MinSize": 2}[k]
+    args = [] if v is None else (list(v) if isinstance(v, list) else [v])
+    return [fc["rate_bits"], fc["cap_height"], fc["proof_of_work_bits"], tag, len(args)] + args + [fc["num_query_rounds"]]
+
+
+def circuit_words(common_json: Union[str, bytes], vkey_json: Union[str, bytes]) -> np.ndarray:
+    """VerifierCircuitData (Types.hs:220-240) as words, from the JSON files it decodes from."""
+    import json
+    c, vk = json.loads(common_json), json.loads(vkey_json)
+    cfg = c["config"]
+    w = [WORDS_CIRCUIT_MAGIC, cfg["num_wires"], cfg["num_routed_wires"], cfg["num_constants"],
+         int(cfg["use_base_arithmetic_gate"]), cfg["security_bits"], cfg["num_challenges"], int(cfg["zero_knowledge"]),
+         int(cfg["randomize_unused_wires"]), cfg["max_quotient_degree_factor"]]
+    w += _fri_config_words(cfg["fri_config"])
+    fp = c["fri_params"]
+    w += _fri_config_words(fp["config"]) + [int(fp["hiding"]), fp["degree_bits"], len(fp["reduction_arity_bits"])]
+    w += list(fp["reduction_arity_bits"])
+    w += [len(c["gates"])]
+    for g in c["gates"]:
+        w += _gate_words(g)
+    si = c["selectors_info"]
+    w += [len(si["selector_indices"])] + list(si["selector_indices"]) + [len(si["groups"])]
+    for g in si["groups"]:
+        w += [g["start"], g["end"]]
+    sv = si.get("selector_vector")
+    w += [0] if sv is None else [1, len(sv)] + list(sv)
+    w += [c["quotient_degree_factor"], c["num_gate_constraints"], c["num_constants"], c["num_public_inputs"]]
+    w += [len(c["k_is"])] + [int(x) % P for x in c["k_is"]]
+    w += [c["num_partial_products"], c["num_lookup_polys"], c["num_lookup_selectors"], len(c["luts"])]
+    for t in c["luts"]:
+        w += [len(t)]
+        for inp, out in t:
+            w += [int(inp), int(out)]
+    cap = vk["constants_sigmas_cap"]
+    w += [len(cap)]
+    for d in cap:
+        w += [int(x) % P for x in d["elements"]]
+    w += [int(x) % P for x in vk["circuit_digest"]["elements"]]
+    return np.array([x & _M64 for x in w], dtype=np.uint64)
+
+
+def proof_words(proof_json: Union[str, bytes]) -> np.ndarray:
+    """ProofWithPublicInputs (Types.hs:245-279) as words, from its JSON."""
+    import json
+    d = json.loads(proof_json)
+    pr = d["proof"]
+    w = [WORDS_PROOF_MAGIC]
+
+    def cap(c):
+        w.append(len(c))
+        for dg in c:
+            w.extend(int(x) % P for x in dg["elements"])
+
+    def exts(v):
+        w.append(len(v))
+        for a, b in v:
+            w.extend((int(a) % P, int(b) % P))
+    cap(pr["wires_cap"])
+    cap(pr["plonk_zs_partial_products_cap"])
+    cap(pr["quotient_polys_cap"])
+    o = pr["openings"]
+    for k in ("constants", "plonk_sigmas", "wires", "plonk_zs", "plonk_zs_next", "partial_products", "quotient_polys",
+              "lookup_zs", "lookup_zs_next"):
+        exts(o[k])
+    fp = pr["opening_proof"]
+    w.append(len(fp["commit_phase_merkle_caps"]))
+    for c in fp["commit_phase_merkle_caps"]:
+        cap(c)
+    w.append(len(fp["query_round_proofs"]))
+    for q in fp["query_round_proofs"]:
+        ep = q["initial_trees_proof"]["evals_proofs"]
+        w.append(len(ep))
+        for leaf, mp in ep:
+            w.append(len(leaf))
+            w.extend(int(x) % P for x in leaf)
+            cap(mp["siblings"])
+        w.append(len(q["steps"]))
+        for st in q["steps"]:
+            exts(st["evals"])
+            cap(st["merkle_proof"]["siblings"])
+    exts(fp["final_poly"]["coeffs"])
+    w.append(int(fp["pow_witness"]) % P)
+    w.append(len(d["public_inputs"]))
+    w.extend(int(x) % P for x in d["public_inputs"])
+    return np.array([x & _M64 for x in w], dtype=np.uint64)

@@ -1,7 +1,9 @@
 """Multi-process sharding (gloo, world_size 2, CPU): the proof-sharding and result
 gathering used for N GPUs (embarrassingly parallel, no data-path
 collective).  The per-shard verification here is the ORACLE (CPU) so the test runs
-without a GPU; on GPUs each rank runs libp2v on its own device."""
+without a GPU; on GPUs each rank runs libp2v on its own device.  The second test drives the
+product's own p2v.verify_sharded (packing, shard bounds, padded all_gather) with the ORACLE
+injected as the per-shard verifier."""
 import os
 import socket
 
@@ -63,3 +65,48 @@ def test_two_rank_gloo_sharded_verification():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert got == expect == [1, 0, 1, -3, 1]
+
+
+def _worker_product(rank, world, port, proofs, common, vkey, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p2v = p2v_module()
+    vk = p2v.VerifierCircuitData.from_json(common, vkey)   # host-only: no GPU needed
+    packed = vk.pack_many(proofs)
+    O = oracle()
+    seen = []
+
+    def shard(rows, s, e):
+        assert rows.shape[0] == e - s and np.array_equal(rows, packed[s:e])
+        seen.append((s, e))
+        return np.array([O.verify_json(common, vkey, proofs[i]) for i in range(s, e)], dtype=np.int8)
+    got = p2v.verify_sharded(vk, packed, rank, world, 0, verify_shard=shard)
+    out.put((rank, seen, got.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_product_verify_sharded_gather_gloo(world):
+    """p2v.verify_sharded itself (the per-rank path of bench.py / multi-GPU hosts) on gloo:
+    every rank verifies exactly its contiguous shard, and every rank ends with the full status
+    vector in batch order (uneven shards: 7 proofs over 2 or 3 ranks)."""
+    gc = gen_circuit(6, 4, 0)
+    kinds = [(1, 1, 0), (1, 5, 2), (2, 2, 0), (1, 4, 1), (2, 3, 0), (1, 6, 4), (2, 9, 0)]
+    proofs = [gc.proof(w, s, flags=f) for w, s, f in kinds]
+    expect = [oracle().verify_json(gc.common, gc.vkey, p) for p in proofs]
+    assert expect == [1, 0, 1, -3, 1, 0, 1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_product, args=(r, world, port, proofs, gc.common, gc.vkey, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    p2v = p2v_module()
+    for rank, seen, got in res:
+        assert seen == [p2v.shard_bounds(len(proofs), world, rank)]
+        assert got == expect

@@ -233,6 +233,35 @@ def test_gpu_multi_device_entry_point(p2v):
         p2v.verify_batch_devices(vk, arr, [0, 99])
 
 
+def test_gpu_multi_device_distinct_devices(p2v):
+    """p2v_verify_batch_devices over distinct GPUs (all visible, up to 8): each shard on its own
+    device must give the single-verifier statuses.  Needs >= 2 GPUs (the driver's multi-GPU
+    node); skipped on a one-GPU box."""
+    n = p2v.device_count()
+    if n < 2:
+        pytest.skip("one GPU visible: distinct-device sharding needs >= 2")
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    pool = vk.pack_many([gc.proof(1, 1), gc.proof(1, 5, flags=2), gc.proof(1, 4, flags=1), gc.proof(2, 2)])
+    idx = np.random.default_rng(4).integers(0, 4, 1001)
+    arr = np.ascontiguousarray(pool[idx])
+    want = p2v.BatchVerifier(vk, 0, len(idx)).run(arr)
+    devs = list(range(min(n, 8)))
+    assert np.array_equal(p2v.verify_batch_devices(vk, arr, devs, chunk=128), want)
+    assert np.array_equal(p2v.verify_batch_devices(vk, arr, devs[::-1] + devs, chunk=64), want)
+
+
+def test_gpu_verify_sharded_single_rank(p2v):
+    """p2v.verify_sharded with the default per-shard BatchVerifier, world 1 (the path every
+    rank of bench.py's N-GPU run takes for its shard)."""
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    pool = vk.pack_many([gc.proof(1, 1), gc.proof(1, 5, flags=2), gc.proof(1, 4, flags=1)])
+    arr = np.ascontiguousarray(pool[np.arange(200) % 3])
+    got = p2v.verify_sharded(vk, arr, 0, 1, 0)
+    assert list(got) == [[1, 0, -3][i % 3] for i in range(200)]
+
+
 def test_gpu_c3_lookup_batch_full_size(p2v):
     """BASELINE configs[2] shape: 65 536 proofs of the lookup circuit (LookupGate +
     LookupTableGate, a 256-entry and a 2^16-entry table) at degree_bits 12 in one batch.

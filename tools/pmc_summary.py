@@ -50,18 +50,37 @@ def main():
     json.dump(out, open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
     vpath = os.path.join(src, "pmc_valu", "run_counter_collection.csv")
     if os.path.exists(vpath):
-        valu = {c: per_kernel(vpath, c) for c in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU")}
-        tot = sum(valu["SQ_INSTS_VALU"].values())
-        vout = {"_note": "rocprofv3 PMC SQ counters per launch (median), bench.py --steps 3 --inflight 1, batch = 4096 std "
-                         "proofs; SQ_INSTS_VALU counts wave-level VALU instructions (x4 cycles each at full rate on a "
-                         "SIMD); share = fraction of all VALU instructions of one verification step; round " + tag}
-        for k in sorted(valu["SQ_INSTS_VALU"]):
-            vout[k] = {c: valu[c].get(k) for c in valu}
-            vout[k]["valu_share"] = round(valu["SQ_INSTS_VALU"][k] / tot, 4)
-        json.dump(vout, open(os.path.join(prof, f"{tag}_pmc_valu.json"), "w"), indent=1)
-        print(json.dumps({k: v["valu_share"] for k, v in vout.items() if not k.startswith("_")}, indent=1))
+        valu_summary(vpath, tag, prof)
     print(json.dumps({k: v for k, v in out.items() if not k.endswith("_KiB")}, indent=1))
 
 
+VALU_COUNTERS = ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU2", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_WAVES",
+                 "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "SQ_BUSY_CYCLES")
+
+
+def valu_summary(vpath, tag, prof):
+    """<tag>_pmc_valu.json: VALU instruction counters per kernel launch (median).  The VALU issue
+    model (measured, profiles/r02_valu_rates.txt + r02_valu_rates_pmc.json): a SIMD issues one
+    VALU instruction per 4-cycle quad, or two in one quad when both are dual-issuable (VOP1/VOP2
+    32-bit ops; SQ_ACTIVE_INST_VALU2 counts those quads), so a launch's VALU issue cycles are
+    4 * (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2); bench.py divides them by 1024 SIMDs x 2.4 GHz x time."""
+    valu = {c: per_kernel(vpath, c) for c in VALU_COUNTERS}
+    valu = {c: v for c, v in valu.items() if v}
+    tot = sum(valu["SQ_INSTS_VALU"].values())
+    vout = {"_note": "rocprofv3 PMC SQ counters per launch (median), bench.py --steps 3 --inflight 1, batch = 4096 std "
+                     "proofs; SQ_INSTS_VALU = wave-level VALU instructions, SQ_ACTIVE_INST_VALU2 = quad-cycles in which "
+                     "two VALU instructions issued; issue_cycles = 4 * (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2); "
+                     "share = fraction of all VALU instructions of one verification step; round " + tag}
+    for k in sorted(valu["SQ_INSTS_VALU"]):
+        vout[k] = {c: valu[c].get(k) for c in valu}
+        vout[k]["issue_cycles"] = 4 * (valu["SQ_INSTS_VALU"][k] - valu.get("SQ_ACTIVE_INST_VALU2", {}).get(k, 0.0))
+        vout[k]["valu_share"] = round(valu["SQ_INSTS_VALU"][k] / tot, 4)
+    json.dump(vout, open(os.path.join(prof, f"{tag}_pmc_valu.json"), "w"), indent=1)
+    print(json.dumps({k: v["valu_share"] for k, v in vout.items() if not k.startswith("_")}, indent=1))
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 2 and sys.argv[1] == "--valu-only":   # tools/pmc_summary.py --valu-only <tag> <csv>
+        valu_summary(sys.argv[3], sys.argv[2], os.path.join(ROOT, "profiles"))
+    else:
+        main()
