@@ -13,7 +13,7 @@
 #include "circuit.hpp"
 #include "dev.h"
 #ifndef P2V_PROOF_MAJOR
-#define P2V_PROOF_MAJOR 0
+#define P2V_PROOF_MAJOR 1   // see devcommon.h ld()
 #endif
 #include "gl.h"
 
@@ -78,7 +78,7 @@ struct p2v_verifier {
   int transcript_mode = 0;          // 0 auto, 1 row, 2 quad (env P2V_TRANSCRIPT)
   int quad_min_batch = 2048;        // auto: quad form from this batch size on
   bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
-  int side_prio = 1;                // side stream at the device's highest priority (env P2V_SIDE_PRIO=0: default priority)
+  int side_prio = 0;                // env P2V_SIDE_PRIO=1: side stream at the device's highest priority (measured: no effect)
   bool debug_sync = false;          // env P2V_DEBUG_SYNC=1: name each launch on stderr and synchronise after it (fault isolation)
   // JSON ingest on the device (p2v_verifier_run_json): the current template and its device
   // form, and buffers grown on demand
@@ -373,7 +373,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   const size_t B = v->Bmax;
   const size_t chw = (size_t)(4 + 7 * d.r + 4 + 2 * d.S + 1 + d.Q + 4);
   if (e == hipSuccess) e = v->in.alloc((size_t)L.words * max_batch * 8);
-  if (e == hipSuccess) e = v->soa.alloc((size_t)L.words * B * 8);
+  if (e == hipSuccess && !P2V_PROOF_MAJOR) e = v->soa.alloc((size_t)L.words * B * 8);   // the transposed batch
   if (e == hipSuccess) e = v->chal.alloc(chw * B * 8);
   if (e == hipSuccess) e = v->leafdig.alloc((size_t)d.Q * d.T * 4 * B * 8);
   if (e == hipSuccess) e = v->mk.alloc((size_t)d.Q * d.T * B);
@@ -389,8 +389,8 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (e == hipSuccess) { for (auto& x : v->ev) { e = hipEventCreate(&x); if (e != hipSuccess) break; } v->timed = e == hipSuccess; }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_p1, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_side, hipEventDisableTiming);
-  // the side stream carries few, long-latency waves (vanishing items, FRI queries) that must
-  // get CU slots while k_merkle floods the device: queue it at the highest priority
+  // the side stream carries few, long-latency waves (vanishing items, FRI queries); a
+  // high-priority queue for it was measured (P2V_SIDE_PRIO=1) and changed nothing
   if (e == hipSuccess) {
     int least = 0, greatest = 0;
     if (v->side_prio && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
@@ -439,14 +439,14 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   // fault isolation (P2V_DEBUG_SYNC=1): each launch is named before it runs and waited for
 #define DBG(name, s_) do { if (v->debug_sync) { fprintf(stderr, "p2v: launched %s\n", name); fflush(stderr); \
     HCK(hipStreamSynchronize(s_)); HCK(hipGetLastError()); fprintf(stderr, "p2v: finished %s\n", name); fflush(stderr); } } while (0)
-  T0(0, st);
 #if P2V_PROOF_MAJOR
-  d.soa = src;   // kernels read the proof-major batch in place (devcommon.h ld())
+  d.soa = src;   // kernels read the proof-major batch in place (devcommon.h ld()); no k_transpose
 #else
+  T0(0, st);
   k_transpose<<<dim3((unsigned)((words + 63) / 64), NPB), 256, 0, st>>>(src, words, (int)n, (uint64_t*)v->soa.p, d.B);
   DBG("k_transpose", st);
-#endif
   T1(0, st);
+#endif
   // phase 1: transcript waves + leaf-hash waves in one launch (the leaf sponges do not
   // depend on the challenges, so they fill the GPU while the serial transcripts run)
   // transcript form: the row form (16 lanes/proof) has the lowest latency, the quad form

@@ -328,7 +328,7 @@ class BatchVerifier:
         buf = (ctypes.c_float * 16)()
         k = lib().p2v_verifier_last_timings(self._h, buf, 16)
         names = lib().p2v_kernel_names().decode().split(",")
-        return {names[i]: float(buf[i]) for i in range(k)}
+        return {names[i]: float(buf[i]) for i in range(k) if buf[i] > 0}   # 0: kernel not launched in this build
 
     def __del__(self):
         try:
