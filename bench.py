@@ -10,12 +10,14 @@ other's Merkle work; the one-at-a-time figure is reported alongside ("serial"). 
 N ranks (torchrun), each verifying its own batch (proofs shard with no data-path
 collective: weak scaling); value = all proofs of all ranks / max-over-ranks time.
 
-Workload: synthetic valid proofs from the degenerate-circuit prover (csrc/gen): standard
-recursion config (degree_bits 12, rate_bits 3, cap_height 4, 28 queries, arity 16, PoW 16,
-135 wires / 80 routed, 14-gate recursion gate set incl. Poseidon + CosetInterpolation),
-D distinct proofs per rank tiled into distinct HBM memory, 1/16 of them corrupted (initial
-Merkle leaf -> -1, last step sibling -> -2).  Every timed batch's statuses are checked
-against the expected vector.
+Workload: synthetic valid proofs from the build's prover (csrc/gen): standard recursion
+config (degree_bits 12, rate_bits 3, cap_height 4, 28 queries, arity 16, PoW 16, 135 wires /
+80 routed, the 14-gate recursion gate set incl. Poseidon + CosetInterpolation).  By default a
+real circuit (gates on rows, selector polynomials, copy constraints, Z / partial products, a
+genuine quotient: every vanishing term non-zero at zeta; --circuit degenerate for the
+gate-filters-0 circuit, which --lookups uses).  D distinct proofs per rank tiled into distinct
+HBM memory, 1/16 of them corrupted (initial Merkle leaf -> -1, last step sibling -> -2).
+Every timed batch's statuses are checked against the expected vector.
 """
 from __future__ import annotations
 
@@ -85,10 +87,13 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_workload(degree_bits, distinct, witnesses, seed_base, threads, lookups=0):
+def make_workload(degree_bits, distinct, witnesses, seed_base, threads, lookups=0, real=False):
+    """real: the generator's real circuit (every gate of the recursion set on rows, selector
+    polynomials, copy constraints, a genuine quotient: every vanishing term non-zero at zeta);
+    else the degenerate circuit (same shapes and the same verifier work, gate filters 0)."""
     from support import generator
     g = generator()
-    gc = g.circuit(degree_bits, 4, lookups, 1, 28, 16)
+    gc = g.circuit(degree_bits, 4, lookups, 1, 28, 16, 0, 1 if real else 0)
     wseeds = [seed_base * 1000 + i + 1 for i in range(witnesses)]
     with cf.ThreadPoolExecutor(threads) as ex:
         list(ex.map(gc.witness, wseeds))
@@ -346,6 +351,9 @@ def main():
     ap.add_argument("--batch", type=int, default=4096, help="proofs per GPU per step")
     ap.add_argument("--distinct", type=int, default=64, help="distinct generated proofs per rank (tiled)")
     ap.add_argument("--witnesses", type=int, default=8)
+    ap.add_argument("--circuit", choices=("real", "degenerate"), default="real",
+                    help="real: gates on rows, copy constraints, genuine quotient (C4's recursion gate set); "
+                         "degenerate: gate filters 0 (required with --lookups: the real prover has no lookup argument)")
     ap.add_argument("--degree-bits", type=int, default=12)
     ap.add_argument("--inflight", type=int, default=2, help="batches in flight per GPU (workspaces/streams)")
     ap.add_argument("--lookups", type=int, default=0,
@@ -388,7 +396,8 @@ def main():
 
     threads = max(1, min(16, (os.cpu_count() or 8)))
     t0 = time.time()
-    gc, proofs = make_workload(args.degree_bits, args.distinct, args.witnesses, rank + 1, threads, args.lookups)
+    real = args.circuit == "real" and not args.lookups
+    gc, proofs = make_workload(args.degree_bits, args.distinct, args.witnesses, rank + 1, threads, args.lookups, real)
     log(f"[rank {rank}] generated {len(proofs)} distinct proofs in {time.time() - t0:.1f}s")
     vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
     info = vk.info
@@ -476,6 +485,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u64 (Goldilocks mod-p integer)", "data": "synthetic",
             "config": {"workload": f"{'C3' if args.lookups else 'C2'}: {B} std-config Plonky2 proofs per GPU per step (degree_bits {info.degree_bits}, "
+                                   f"{'real circuit of the recursion gate set, ' if real else 'degenerate circuit, '}"
                                    f"28 FRI queries, arity 16, deg-2 ext{', lookups: 256 + 65536-entry tables' if args.lookups > 1 else (', lookups' if args.lookups else '')}), "
                                    f"{len(proofs)} distinct tiled, 1/16 corrupted, device-resident",
                        "global_batch": B * world, "degree_bits": info.degree_bits, "parallelism": f"proof-sharded x{world}",

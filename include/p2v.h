@@ -209,6 +209,9 @@ int  p2v_verify_batch_devices(const p2v_circuit* c, const uint64_t* proofs, size
  *   op 1: out[12i..] = Poseidon permutation of a[12i..]     (Hash/Poseidon.hs:42-46)
  *   op 2: out[12i..12i+4) = compress form: words 8..11 of a[12i..] taken as 0, words 0..3 of
  *         the permutation returned, the rest 0               (Hash/Merkle.hs:21-24)
+ *   op 4: out[12i..] = M a[12i..] + (b[0..12) + 2^32 b[12..24)) mod p, not canonicalised: one MDS
+ *         layer with the next round's constants as the permutation computes it (the row
+ *         reduction's rare carry fix-up included; b, 24 words, shared by all items) (Poseidon.hs:100-101)
  * Inputs may be any u64 (values >= p are congruent, as the reference reads them).
  * Test hook for the parity suite (edge values the synthetic proofs never produce). */
 int  p2v_selftest(int device, int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n);

@@ -592,6 +592,10 @@ static int pack_json_into(p2v_verifier* v, const char* blob, const uint64_t* off
     HCK(put(v->j_skel, skel.data(), skel.size()));
     HCK(put(v->j_tok, tok.data(), tok.size() * sizeof(int32_t)));
     v->skel_len = (int64_t)skel.size(); v->ntok = (int64_t)tok.size();
+  } else if (fresh || !v->have_tmpl) {
+    // a new template without a device form (or none at all): drop the previous template's
+    // device form, so no later batch pairs it with this host template
+    v->skel_len = 0; v->ntok = 0;
   }
   std::vector<int8_t> okf(n, 0);
   if (dev_ok && v->ntok > 0) {
@@ -652,7 +656,7 @@ int p2v_verifier_run_json(p2v_verifier* v, const char* blob, const uint64_t* off
 }
 
 int p2v_selftest(int device, int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n) {
-  if (op < 0 || op > 3 || (n && (!a || !out || ((op == 0 || op == 3) && !b)))) return fail(P2V_E_ARG, "bad op / null argument");
+  if (op < 0 || op > 4 || (n && (!a || !out || ((op == 0 || op == 3 || op == 4) && !b)))) return fail(P2V_E_ARG, "bad op / null argument");
   const int ndev = p2v_device_count();
   if (ndev == 0) return fail(P2V_E_NODEVICE, "no HIP device");
   if (device < 0 || device >= ndev) return fail(P2V_E_ARG, "bad device index");
@@ -663,10 +667,11 @@ int p2v_selftest(int device, int op, const uint64_t* a, const uint64_t* b, uint6
   DevBuf da, db, dout;
   auto cleanup = [&]() { da.free_(); db.free_(); dout.free_(); };
   hipError_t e = da.alloc(n * w * 8);
-  if (e == hipSuccess) e = db.alloc(fm ? n * 8 : 16);
+  if (e == hipSuccess) e = db.alloc(fm ? n * 8 : op == 4 ? 24 * 8 : 16);
   if (e == hipSuccess) e = dout.alloc(n * w * 8);
   if (e == hipSuccess) e = hipMemcpy(da.p, a, n * w * 8, hipMemcpyHostToDevice);
   if (e == hipSuccess && fm) e = hipMemcpy(db.p, b, n * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess && op == 4) e = hipMemcpy(db.p, b, 24 * 8, hipMemcpyHostToDevice);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_selftest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, op, (const uint64_t*)da.p,
                        (const uint64_t*)db.p, (uint64_t*)dout.p, (int64_t)n);

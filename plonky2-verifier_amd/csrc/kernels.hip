@@ -499,7 +499,8 @@ extern "C" __global__ void __launch_bounds__(256) k_status(DevCircuit c, int8_t*
 // multiply form (gl::mul_nc_dev_v<2>, canonicalised), op 1 the
 // Poseidon permutation (permute_dev, Hash/Poseidon.hs:42-46; a = n states of 12 words),
 // op 2 the 2-to-1 compression form (permute_dev(s, zh, gm = words 0..3), Hash/Merkle.hs:21-24;
-// a = n states whose words 8..11 are ignored and taken as 0).  One lane per item.
+// a = n states whose words 8..11 are ignored and taken as 0), op 4 one MDS layer + constants
+// (the permutation's row reduction with its grouped carry fix-up).  One lane per item.
 extern "C" __global__ void __launch_bounds__(256) k_selftest(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -508,6 +509,24 @@ extern "C" __global__ void __launch_bounds__(256) k_selftest(int op, const uint6
   } else if (op == 3) {
 #if defined(__HIP_DEVICE_COMPILE__)
     out[i] = gl::canon(gl::mul_nc_dev_v<2>(a[i], b[i]));
+#endif
+  } else if (op == 4) {
+    // one MDS layer plus the next round's constants, exactly as the permutation runs it
+    // (poseidon.h: 32-bit-half accumulators, the rare carry fix-up in one uniform branch per
+    // group of 4 rows); b = the constants' halves kl[12], kh[12], shared by every item
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint64_t st[12], t[12], kl[12], kh[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) { st[k] = a[12 * i + k]; kl[k] = b[k]; kh[k] = b[12 + k]; }
+#if P2V_MDS_BRANCH == 2
+    p2::dv::mds_group<0>(st, t, kl, kh);
+    p2::dv::mds_group<4>(st, t, kl, kh);
+    p2::dv::mds_group<8>(st, t, kl, kh);
+#else
+    p2::dv::mds_rows<0, 12>(st, t, kl, kh);
+#endif
+#pragma unroll
+    for (int k = 0; k < 12; k++) out[12 * i + k] = t[k];
 #endif
   } else {
     uint64_t s[12];

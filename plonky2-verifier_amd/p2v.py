@@ -353,7 +353,7 @@ def device_selftest(op: int, a: np.ndarray, b: Optional[np.ndarray] = None, devi
     returned) on `device`."""
     a = np.ascontiguousarray(a, dtype=np.uint64)
     n = a.shape[0]
-    out = np.zeros_like(a)
+    out = np.zeros_like(a)   # op 4: one MDS layer + constants b = [kl[12], kh[12]] (include/p2v.h)
     bb = np.ascontiguousarray(b, dtype=np.uint64) if b is not None else None
     _check(lib().p2v_selftest(device, op, a.ctypes.data, bb.ctypes.data if bb is not None else None, out.ctypes.data, n))
     return out

@@ -478,3 +478,67 @@ def test_gpu_poseidon_permutation_vs_oracle(p2v):
         assert [int(x) for x in full[i]] == exp, i
         expc = O.permute([int(x) % P for x in st[:8]] + [0] * 4)
         assert [int(x) for x in comp[i][:4]] == expc[:4], i
+
+
+def _mds_fixup_cases(rng, n=512):
+    """States that drive the MDS row reduction's rare carry fix-up (poseidon.h reduce_rows /
+    mds_group: it fires when a row's high-half accumulator has its low 32 bits above
+    2^32 - 2^11, ~2^-21 per row for random data).  For each state a random subset of rows is
+    aimed at low half 2^32 - 1 (the fix-up fires) or 2^32 - 2^11 (just below the threshold) by
+    solving for some input words' high halves mod 2^32; the other rows stay random."""
+    M32 = (1 << 32) - 1
+    circ = [17, 15, 41, 16, 2, 28, 13, 13, 39, 18, 34, 20]
+
+    def c(i, j):
+        return circ[(j - i) % 12] + (8 if i == j == 0 else 0)
+    kl = [int(x) for x in rng.integers(0, 1 << 32, 12, dtype=np.uint64)]
+    kh = [int(x) for x in rng.integers(0, 1 << 32, 12, dtype=np.uint64)]
+    states, hits = [], []
+    while len(states) < n:
+        rows = sorted(rng.choice(12, size=int(rng.integers(1, 4)), replace=False).tolist())
+        cols = sorted(rng.choice(12, size=len(rows), replace=False).tolist())
+        s = [int(x) for x in rng.integers(0, (1 << 64) - (1 << 32), 12, dtype=np.uint64)]
+        target = [M32 if rng.integers(2) else (1 << 32) - (1 << 11) for _ in rows]
+        # A x = b (mod 2^32) over the chosen columns' high halves; Gaussian elimination with odd pivots
+        A = [[c(i, j) for j in cols] + [(target[k] - kh[i] - sum(c(i, j) * (s[j] >> 32) for j in range(12) if j not in cols)) & M32]
+             for k, i in enumerate(rows)]
+        m, ok = len(rows), True
+        for col in range(m):
+            piv = next((r for r in range(col, m) if A[r][col] & 1), None)
+            if piv is None:
+                ok = False
+                break
+            A[col], A[piv] = A[piv], A[col]
+            inv = pow(A[col][col], -1, 1 << 32)
+            A[col] = [(x * inv) & M32 for x in A[col]]
+            for r in range(m):
+                if r != col and A[r][col]:
+                    f = A[r][col]
+                    A[r] = [(x - f * y) & M32 for x, y in zip(A[r], A[col])]
+        if not ok:
+            continue
+        for k, j in enumerate(cols):
+            s[j] = (A[k][m] << 32) | (s[j] & M32)
+        states.append(s)
+        hits.append([i for i, t in zip(rows, target) if t == M32])
+    return states, kl, kh, hits, c
+
+
+def test_gpu_mds_layer_carry_fixup(p2v):
+    """the grouped MDS carry fix-up (P2V_MDS_BRANCH 2) is reached deterministically:
+    crafted states fire it in 1-3 rows of a group and leave the group's other rows alone (and
+    near-misses just below the threshold); p2v_selftest op 4 runs one MDS layer exactly as the
+    permutation does, compared with exact integer arithmetic."""
+    P = (1 << 64) - (1 << 32) + 1
+    rng = np.random.default_rng(21)
+    states, kl, kh, hits, c = _mds_fixup_cases(rng)
+    a = np.array(states, dtype=np.uint64)
+    out = p2v.device_selftest(4, a, np.array(kl + kh, dtype=np.uint64))
+    fired = 0
+    for s, o in zip(states, out):
+        for i in range(12):
+            al = sum(c(i, j) * (s[j] & 0xFFFFFFFF) for j in range(12)) + kl[i]
+            ah = sum(c(i, j) * (s[j] >> 32) for j in range(12)) + kh[i]
+            assert int(o[i]) % P == (al + (ah << 32)) % P, (i, s)
+            fired += ((al + (ah >> 32) * 0xFFFFFFFF) >> 32) + (ah & 0xFFFFFFFF) >= 1 << 32   # the carry of reduce_rows
+    assert fired > 300   # the fix-up branch really ran (hundreds of rows, in every group)
