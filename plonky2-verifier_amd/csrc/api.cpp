@@ -434,7 +434,8 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   const int NPB = d.B / 64;
   const bool tm = v->timed;
   hipStream_t sd = v->single_stream ? st : v->side;
-#define T0(k, s_) do { if (tm) HCK(hipEventRecord(v->ev[2 * (k)], s_)); } while (0)
+  uint32_t timed_mask = 0;   // slots recorded in this run (only those are read back)
+#define T0(k, s_) do { if (tm) { HCK(hipEventRecord(v->ev[2 * (k)], s_)); timed_mask |= 1u << (k); } } while (0)
 #define T1(k, s_) do { if (tm) HCK(hipEventRecord(v->ev[2 * (k) + 1], s_)); } while (0)
   // fault isolation (P2V_DEBUG_SYNC=1): each launch is named before it runs and waited for
 #define DBG(name, s_) do { if (v->debug_sync) { fprintf(stderr, "p2v: launched %s\n", name); fflush(stderr); \
@@ -509,7 +510,14 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   if (!(flags & P2V_FLAG_NO_SYNC) || !(flags & P2V_FLAG_RESULT_DEVICE)) {
     HCK(hipStreamSynchronize(st));
     if (!(flags & P2V_FLAG_RESULT_DEVICE)) memcpy(results, v->h_res, n);
-    if (tm) for (int k = 0; k < kNumKernels; k++) { float ms = 0; if (hipEventElapsedTime(&ms, v->ev[2 * k], v->ev[2 * k + 1]) == hipSuccess) v->last_ms[k] = ms; }
+    if (tm) {
+      for (int k = 0; k < kNumKernels; k++) {
+        float ms = 0;
+        if ((timed_mask >> k) & 1u) { if (hipEventElapsedTime(&ms, v->ev[2 * k], v->ev[2 * k + 1]) == hipSuccess) v->last_ms[k] = ms; }
+        else v->last_ms[k] = 0;   // not launched in this build / run
+      }
+      (void)hipGetLastError();   // a failed timing query must not surface as the next call's error
+    }
   }
   return P2V_OK;
 }
