@@ -69,8 +69,10 @@ typedef struct p2v_circuit_info {
   int32_t num_gates;
   int64_t proof_words;        /* u64 words of one packed proof                    */
   int64_t trace_words;        /* u64 words of one debug trace (see p2v_trace_layout) */
-  int32_t oracle_widths[4];   /* leaf widths of the 4 initial oracles  Plonk/FRI.hs:56-65 */
+  int32_t oracle_widths[4];   /* data widths of the 4 initial oracles  Plonk/FRI.hs:56-65 */
   int32_t step_arity_bits[8];
+  int32_t leaf_widths[4];     /* packed leaf widths: oracle_widths + salts (P2V_EXT_HIDING), else equal */
+  uint32_t ext;               /* the P2V_EXT_* flags the circuit was created with */
 } p2v_circuit_info;
 
 /* ---- circuits (host-only, no GPU needed) --------------------------------------- */
@@ -78,6 +80,29 @@ int  p2v_circuit_from_json(const char* common_json, size_t common_len,
                            const char* vkey_json,   size_t vkey_len,
                            p2v_circuit** out);
 void p2v_circuit_free(p2v_circuit* c);
+
+/* ---- opt-in plonky2 semantics the reference does not implement ------
+ * With ext = 0 (p2v_circuit_from_json / _from_words) every entry point follows the reference
+ * exactly.  The flags below switch single conventions to what plonky2's own verifier does, for
+ * circuits the reference rejects; nothing in the reference pins them (parity unpinned).
+ *   P2V_EXT_PARAMS_ARITIES  the FRI steps are fri_params.reduction_arity_bits, as plonky2's
+ *                           verifier reads them, instead of expanding the strategy from
+ *                           degree_bits (Plonk/FRI.hs:337-354, :378); MinSize (an `error` in the
+ *                           reference, Plonk/FRI.hs:342) is then accepted
+ *   P2V_EXT_HIDING          when fri_params.hiding: the wires, zs/partial-products and quotient
+ *                           leaves carry SALT_SIZE = 4 trailing salt elements, hashed into the leaf
+ *                           and left out of combineInitial (plonky2 FriInitialTreeProof::
+ *                           unsalted_evals; the reference errors in buildListOracle, Plonk/FRI.hs:74)
+ *   P2V_EXT_HASH_OR_NOOP    Merkle leaves (initial and FRI step) of <= 4 elements are the digest
+ *                           itself, zero-padded (plonky2 hash_or_noop; the reference always
+ *                           sponges, Hash/Merkle.hs:27-28, commentary/FRI.md:14) */
+#define P2V_EXT_PARAMS_ARITIES 1u
+#define P2V_EXT_HIDING         2u
+#define P2V_EXT_HASH_OR_NOOP   4u
+#define P2V_EXT_PLONKY2        7u   /* all of the above */
+int  p2v_circuit_from_json_ex(const char* common_json, size_t common_len,
+                              const char* vkey_json,   size_t vkey_len,
+                              uint32_t ext, p2v_circuit** out);
 int  p2v_circuit_get_info(const p2v_circuit* c, p2v_circuit_info* info);
 
 /* Pack one ProofWithPublicInputs JSON (Types.hs:245-254) into the circuit's fixed
@@ -139,10 +164,24 @@ int  p2v_pack_proofs_json(const p2v_circuit* c, const char* const* jsons, const 
 /* VerifierCircuitData from its word encoding (same validation and errors as
  * p2v_circuit_from_json).  Replaces: MkVerifierCircuitData of decoded values (Types.hs:220-224). */
 int  p2v_circuit_from_words(const uint64_t* words, size_t n, p2v_circuit** out);
+int  p2v_circuit_from_words_ex(const uint64_t* words, size_t n, uint32_t ext, p2v_circuit** out);
 /* ProofWithPublicInputs from its word encoding into the circuit's packed layout (dst holds
  * info.proof_words u64); P2V_E_PARSE on a malformed encoding, P2V_E_SHAPE on list lengths the
  * circuit does not imply (as p2v_pack_proof_json). */
 int  p2v_pack_proof_words(const p2v_circuit* c, const uint64_t* words, size_t n, uint64_t* dst);
+
+/* ---- plonky2's binary proof serialization (not in the reference,
+ * README.md:27) -----------------------------------------------------------------------
+ * One ProofWithPublicInputs as plonky2's `to_bytes` writes it (Write::write_proof_with_public_inputs):
+ * u64 little-endian words (F reduced mod p), caps as 2^cap_height hashes, Merkle proofs as a u8
+ * sibling count then the hashes, the circuit-sized vectors without lengths, in the order
+ * wires_cap, zs_pp_cap, quotient_cap, openings (constants, plonk_sigmas, wires, plonk_zs,
+ * plonk_zs_next, lookup_zs, lookup_zs_next, partial_products, quotient_polys), commit caps, query
+ * rounds (4 x (leaf, proof), steps x (evals, proof)), final_poly, pow_witness, then the public
+ * inputs (the remaining words, or a u64 count and the words).  Packed into the circuit's layout as
+ * p2v_pack_proof_json does; P2V_E_PARSE when truncated, P2V_E_SHAPE on a sibling count or public
+ * input count the circuit does not imply.  Parity unpinned (no binary fixture offline). */
+int  p2v_pack_proof_bytes(const p2v_circuit* c, const uint8_t* bytes, size_t n, uint64_t* dst);
 
 /* ---- verification (GPU) ------------------------------------------------------------ */
 #define P2V_FLAG_INPUT_DEVICE  1u  /* `proofs` is a device pointer on the verifier's device  */

@@ -165,8 +165,11 @@ static void compress(const F* x, const F* y, F out[4]) {
 
 /* reconstructMerkleRoot / checkMerkleProof, Hash/Merkle.hs:27-42 */
 static int check_merkle(const F (*cap)[4], int ncap, long idx, const F* leaf, long nleaf,
-                        const F (*sib)[4], int nsib) {
-  F cur[4]; sponge(leaf, nleaf, cur);
+                        const F (*sib)[4], int nsib, int noop) {
+  F cur[4];
+  if (noop && nleaf <= 4) {   /* P2V_EXT_HASH_OR_NOOP: plonky2 hash_or_noop, the leaf zero-padded */
+    memset(cur, 0, sizeof cur); memcpy(cur, leaf, (size_t)nleaf * sizeof(F));
+  } else sponge(leaf, nleaf, cur);
   for (int k = 0; k < nsib; k++) {
     F nx[4];
     if ((idx & 1) == 0) compress(cur, sib[k], nx); else compress(sib[k], cur, nx);
@@ -186,6 +189,8 @@ typedef struct {
   int num_wires, num_routed, num_const_cfg, r, max_qdf;
   int rate_bits, cap_height, pow_bits, nqueries;
   int strat;  /* 0 ConstantArityBits, 1 Fixed, 2 MinSize */
+  int hiding; int* params_ar; int nparams_ar;   /* fri_params.hiding, .reduction_arity_bits (Types.hs:153-155) */
+  unsigned ext;                                  /* P2V_EXT_* opt-in plonky2 conventions (include/p2v.h) */
   int strat_a, strat_b; int* fixed; int nfixed;
   int degree_bits;
   gate_t* gates; int ngates;
@@ -379,12 +384,19 @@ static void load_circuit(circuit_t* C, const oj* common, const oj* vkey) {
     const oj* fx = arr(rs->items[0]); C->strat = 1; C->nfixed = (int)fx->n;
     C->fixed = (int*)aalloc(m, (fx->n + 1) * sizeof(int));
     for (size_t i = 0; i < fx->n; i++) C->fixed[i] = (int)j_int(fx->items[i]);
-  } else if (!strcmp(rs->keys[0], "MinSize")) { C->strat = 2; }
+  } else if (!strcmp(rs->keys[0], "MinSize")) {   /* Maybe Log2: null or a number */
+    C->strat = 2;
+    if (rs->items[0]->kind != OJ_NULL) (void)j_int(rs->items[0]);
+  }
   else fail(P2V_ERR_PARSE, "unrecognized FRI reduction strategy");
   const oj* fp = req(common, "fri_params");
-  (void)j_bool(req(fp, "hiding"));
+  C->hiding = j_bool(req(fp, "hiding"));
   C->degree_bits = (int)j_int(req(fp, "degree_bits"));
-  (void)arr(req(fp, "reduction_arity_bits"));
+  {
+    const oj* ra = arr(req(fp, "reduction_arity_bits"));
+    C->nparams_ar = (int)ra->n; C->params_ar = (int*)aalloc(m, (ra->n + 1) * sizeof(int));
+    for (size_t i = 0; i < ra->n; i++) C->params_ar[i] = (int)j_int(ra->items[i]);
+  }
   (void)req(fp, "config");
   const oj* gs = arr(req(common, "gates"));
   C->ngates = (int)gs->n; C->gates = (gate_t*)aalloc(m, (gs->n + 1) * sizeof(gate_t));
@@ -944,6 +956,9 @@ static void eval_all_constraints(arena* m, const circuit_t* C, const proof_t* P,
 
 /* ===================================================================== FRI
  * Plonk/FRI.hs:56-407 */
+/* SALT_SIZE trailing salts of the wires / zs / quotient leaves under P2V_EXT_HIDING (plonky2
+ * FriInitialTreeProof::unsalted_evals); the reference has none (Plonk/FRI.hs:56-75) */
+static int leaf_salt(const circuit_t* C, int t) { return (C->ext & 2u) && C->hiding && t > 0 ? 4 : 0; }
 static int oracle_width(const circuit_t* C, int t) {   /* oracleWidths :56-65 */
   switch (t) {
     case 0: return C->num_constants + C->num_routed;
@@ -954,6 +969,10 @@ static int oracle_width(const circuit_t* C, int t) {   /* oracleWidths :56-65 */
 }
 static int expand_strategy(const circuit_t* C, int* arities) {   /* expandReductionStrategy :337-354 */
   int n = 0;
+  if (C->ext & 1u) {   /* P2V_EXT_PARAMS_ARITIES: plonky2 reads fri_params.reduction_arity_bits */
+    for (int i = 0; i < C->nparams_ar && i < 64; i++) arities[n++] = C->params_ar[i];
+    return n;
+  }
   if (C->strat == 0) { int logn = C->degree_bits; while (logn > C->strat_b) { if (n >= 64) fail(P2V_ERR_CIRCUIT, "reduction strategy does not terminate"); arities[n++] = C->strat_a; logn -= C->strat_a; } }
   else if (C->strat == 1) { for (int i = 0; i < C->nfixed && i < 64; i++) arities[n++] = C->fixed[i]; }
   else fail(P2V_ERR_CIRCUIT, "reduction strategy not implemented");
@@ -995,15 +1014,17 @@ static void check_query_round(const circuit_t* C, const proof_t* P, const chal_t
   int ncaps[4] = { C->ncs_cap, P->nwc, P->nzc, P->nqc };
   for (int t = 0; t < 4; t++) if (ncaps[t] != (1 << C->cap_height)) fail(P2V_ERR_SHAPE, "validateMerkleCapLength: cap has wrong size");
   int merkle_ok = 1;   /* and [...] short-circuits */
-  for (int t = 0; t < 4 && (merkle_ok || !strict); t++) if (!check_merkle(caps[t], ncaps[t], idx, R->init[t].leaf, R->init[t].nleaf, (const F (*)[4])R->init[t].sib, R->init[t].nsib)) merkle_ok = 0;
+  const int noop = (C->ext & 4u) != 0;
+  for (int t = 0; t < 4 && (merkle_ok || !strict); t++) if (!check_merkle(caps[t], ncaps[t], idx, R->init[t].leaf, R->init[t].nleaf, (const F (*)[4])R->init[t].sib, R->init[t].nsib, noop)) merkle_ok = 0;
   if (!merkle_ok) { res->code = P2V_ERR_INITIAL_MERKLE; if (strict) return; }
-  for (int t = 0; t < 4; t++) if (R->init[t].nleaf != oracle_width(C, t)) fail(P2V_ERR_SHAPE, "buildListOracle: list size do not match the expected");
+  for (int t = 0; t < 4; t++) if (R->init[t].nleaf != oracle_width(C, t) + leaf_salt(C, t)) fail(P2V_ERR_SHAPE, "buildListOracle: list size do not match the expected");
   /* combineInitial :151-207 */
   int r = C->r;
   int npp = (C->num_routed + C->qdf - 1) / C->qdf;
   if (r * (npp + C->nlp) != oracle_width(C, 2)) fail(P2V_ERR_CIRCUIT, "combineInitial: sanity check failed");
   const F* oc = R->init[0].leaf; const F* ow = R->init[1].leaf; const F* opl = R->init[2].leaf; const F* oq = R->init[3].leaf;
-  int noc = R->init[0].nleaf, now = R->init[1].nleaf, npl = R->init[2].nleaf, noq = R->init[3].nleaf;
+  int noc = R->init[0].nleaf - leaf_salt(C, 0), now = R->init[1].nleaf - leaf_salt(C, 1),
+      npl = R->init[2].nleaf - leaf_salt(C, 2), noq = R->init[3].nleaf - leaf_salt(C, 3);   /* unsalted */
   int nppo = r * npp < npl ? r * npp : npl;
   int len1 = noc + now + nppo + noq + (npl - nppo);
   int len2 = (r < nppo ? r : nppo) + (npl - nppo);
@@ -1030,7 +1051,7 @@ static void check_query_round(const circuit_t* C, const proof_t* P, const chal_t
     long nidx = qidx >> ab;
     F* flat = (F*)malloc((2 * S->nevals + 1) * 8);
     for (int i = 0; i < S->nevals; i++) { flat[2 * i] = S->evals[i].a; flat[2 * i + 1] = S->evals[i].b; }
-    int ok_m = check_merkle((const F (*)[4])P->ccaps[s], P->nccap[s], nidx, flat, 2 * S->nevals, (const F (*)[4])S->sib, S->nsib);
+    int ok_m = check_merkle((const F (*)[4])P->ccaps[s], P->nccap[s], nidx, flat, 2 * S->nevals, (const F (*)[4])S->sib, S->nsib, noop);
     free(flat);
     if (res->code == 1 && !ok_m) { res->code = P2V_ERR_STEP_MERKLE; if (strict) return; }
     long pos = qidx % arity;
@@ -1182,6 +1203,8 @@ or_circuit* or_circuit_load(const char* common, size_t clen, const char* vkey, s
   return oc;
 }
 void or_circuit_free(or_circuit* c) { if (c) { afree(&c->c.mem); free(c); } }
+/* opt-in plonky2 conventions (P2V_EXT_* of include/p2v.h); 0 = the reference's */
+void or_circuit_set_ext(or_circuit* c, unsigned ext) { c->c.ext = ext; }
 
 or_proof* or_proof_load(const char* proof, size_t plen) {
   or_proof* volatile op = (or_proof*)calloc(1, sizeof(or_proof));

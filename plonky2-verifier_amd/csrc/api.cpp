@@ -19,6 +19,8 @@
 
 extern "C" __global__ void k_transpose(const uint64_t*, int64_t, int, uint64_t*, int);
 extern "C" __global__ void k_phase1(DevCircuit, int, int);
+extern "C" __global__ void k_transcript(DevCircuit, int);
+extern "C" __global__ void k_leaf(DevCircuit);
 extern "C" __global__ void k_merkle(DevCircuit);
 extern "C" __global__ void k_fri(DevCircuit);
 extern "C" __global__ void k_vanish(DevCircuit);
@@ -36,9 +38,10 @@ namespace {
 thread_local std::string g_err;
 int fail(int code, const std::string& msg) { g_err = msg; return code; }
 
-// per-kernel timing slots; k_fri and k_vanish run on the side stream concurrently with k_merkle
-const char* kKernelNames = "k_transpose,k_phase1,k_merkle,k_fri,k_vanish,k_status,k_vanish_final,k_lut";
-constexpr int kNumKernels = 8;
+// per-kernel timing slots; k_fri and k_vanish run on the side stream, concurrently with k_merkle
+// (k_leaf + k_transcript: the split form of k_phase1, env P2V_PHASE1=split, measurement only)
+const char* kKernelNames = "k_transpose,k_phase1,k_merkle,k_fri,k_vanish,k_status,k_vanish_final,k_lut,k_leaf,k_transcript";
+constexpr int kNumKernels = 10;
 
 struct DevBuf {
   void* p = nullptr;
@@ -71,7 +74,7 @@ struct p2v_verifier {
   DevBuf in, soa, chal, leafdig, mk, fbits, qvals, van, vparts, lutre, lutpart, res, trace;
   DevBuf t_cs, t_kis, t_gkind, t_gpar, t_ggrp, t_gwoff, t_w, t_gs, t_ge, t_lin, t_lout, t_loff, t_llen, t_tw, t_ops, t_vit, t_rin, t_rout, t_roff, t_rch, t_pbase;
   hipEvent_t ev[2 * kNumKernels];   // start/end per kernel
-  hipEvent_t dep_p1 = nullptr, dep_side = nullptr;
+  hipEvent_t dep_p1 = nullptr, dep_side = nullptr, dep_tr = nullptr;
   hipStream_t side = nullptr;
   float last_ms[kNumKernels] = {0};
   bool timed = false;
@@ -79,6 +82,9 @@ struct p2v_verifier {
   int quad_min_batch = 2048;        // auto: quad form from this batch size on
   bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
   int side_prio = 0;                // env P2V_SIDE_PRIO=1: side stream at the device's highest priority (measured: no effect)
+  bool split_phase1 = false;        // env P2V_PHASE1=split: k_transcript (side stream) + k_leaf instead of k_phase1.
+                                    // Measured (profiles/r02_phase1_split.txt): serial 0.94x, pipelined 1.00x; the
+                                    // transcript waves, latency-bound, stretch to 2.9 ms beside k_leaf
   bool debug_sync = false;          // env P2V_DEBUG_SYNC=1: name each launch on stderr and synchronise after it (fault isolation)
   // JSON ingest on the device (p2v_verifier_run_json): the current template and its device
   // form, and buffers grown on demand
@@ -98,12 +104,18 @@ const char* p2v_version(void) { return "p2v 0.1.0 (gfx950)"; }
 const char* p2v_kernel_names(void) { return kKernelNames; }
 
 int p2v_circuit_from_json(const char* common_json, size_t common_len, const char* vkey_json, size_t vkey_len, p2v_circuit** out) {
+  return p2v_circuit_from_json_ex(common_json, common_len, vkey_json, vkey_len, 0, out);
+}
+
+int p2v_circuit_from_json_ex(const char* common_json, size_t common_len, const char* vkey_json, size_t vkey_len, uint32_t ext,
+                             p2v_circuit** out) {
   if (!common_json || !vkey_json || !out) return fail(P2V_E_ARG, "null argument");
+  if (ext & ~P2V_EXT_PLONKY2) return fail(P2V_E_ARG, "unknown P2V_EXT_* flag");
   try {
     JVal cj = parse_json(common_json, common_len);
     JVal vj = parse_json(vkey_json, vkey_len);
     auto* pc = new p2v_circuit();
-    pc->c = parse_circuit(cj, vj);
+    try { pc->c = parse_circuit(cj, vj, ext); } catch (...) { delete pc; throw; }
     *out = pc;
     return P2V_OK;
   } catch (const ParseError& e) { return fail(P2V_E_PARSE, e.what()); }
@@ -112,10 +124,15 @@ int p2v_circuit_from_json(const char* common_json, size_t common_len, const char
 }
 
 int p2v_circuit_from_words(const uint64_t* words, size_t n, p2v_circuit** out) {
+  return p2v_circuit_from_words_ex(words, n, 0, out);
+}
+
+int p2v_circuit_from_words_ex(const uint64_t* words, size_t n, uint32_t ext, p2v_circuit** out) {
   if (!words || !out) return fail(P2V_E_ARG, "null argument");
+  if (ext & ~P2V_EXT_PLONKY2) return fail(P2V_E_ARG, "unknown P2V_EXT_* flag");
   try {
     auto* pc = new p2v_circuit();
-    try { pc->c = parse_circuit_words(words, n); } catch (...) { delete pc; throw; }
+    try { pc->c = parse_circuit_words(words, n, ext); } catch (...) { delete pc; throw; }
     *out = pc;
     return P2V_OK;
   } catch (const ParseError& e) { return fail(P2V_E_PARSE, e.what()); }
@@ -127,6 +144,16 @@ int p2v_pack_proof_words(const p2v_circuit* pc, const uint64_t* words, size_t n,
   if (!pc || !words || !dst) return fail(P2V_E_ARG, "null argument");
   try {
     pack_proof_words(pc->c, words, n, dst);
+    return P2V_OK;
+  } catch (const ShapeError& e) { return fail(P2V_E_SHAPE, e.what()); }
+  catch (const ParseError& e) { return fail(P2V_E_PARSE, e.what()); }
+  catch (const std::exception& e) { return fail(P2V_E_PARSE, e.what()); }
+}
+
+int p2v_pack_proof_bytes(const p2v_circuit* pc, const uint8_t* bytes, size_t n, uint64_t* dst) {
+  if (!pc || !bytes || !dst) return fail(P2V_E_ARG, "null argument");
+  try {
+    pack_proof_bytes(pc->c, bytes, n, dst);
     return P2V_OK;
   } catch (const ShapeError& e) { return fail(P2V_E_SHAPE, e.what()); }
   catch (const ParseError& e) { return fail(P2V_E_PARSE, e.what()); }
@@ -145,7 +172,8 @@ int p2v_circuit_get_info(const p2v_circuit* pc, p2v_circuit_info* info) {
   info->num_openings_this = (int)c.L.n_this; info->num_openings_next = (int)c.L.n_next;
   info->has_lookups = c.lut_in.empty() ? 0 : 1; info->num_gates = (int)c.gates.size();
   info->proof_words = c.L.words; info->trace_words = c.trace_words;
-  for (int t = 0; t < 4; t++) info->oracle_widths[t] = c.oracle_width[t];
+  for (int t = 0; t < 4; t++) { info->oracle_widths[t] = c.oracle_width[t]; info->leaf_widths[t] = c.leaf_width[t]; }
+  info->ext = c.ext;
   for (size_t s = 0; s < c.arities.size() && s < 8; s++) info->step_arity_bits[s] = c.arities[s];
   return P2V_OK;
 }
@@ -224,6 +252,7 @@ void p2v_verifier_free(p2v_verifier* v) {
   if (v->timed) for (auto& e : v->ev) (void)hipEventDestroy(e);
   if (v->dep_p1) (void)hipEventDestroy(v->dep_p1);
   if (v->dep_side) (void)hipEventDestroy(v->dep_side);
+  if (v->dep_tr) (void)hipEventDestroy(v->dep_tr);
   if (v->side) (void)hipStreamDestroy(v->side);
   if (v->h_res) (void)hipHostFree(v->h_res);
   delete v;
@@ -242,6 +271,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (const char* ss = getenv("P2V_SINGLE_STREAM")) v->single_stream = ss[0] == '1';
   if (const char* sp = getenv("P2V_SIDE_PRIO")) v->side_prio = sp[0] == '1';
   if (const char* ds = getenv("P2V_DEBUG_SYNC")) v->debug_sync = ds[0] == '1';
+  if (const char* f1 = getenv("P2V_PHASE1")) v->split_phase1 = !strcmp(f1, "split");
   if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : 0;
   DevCircuit& d = v->dc;
   memset(&d, 0, sizeof d);
@@ -250,7 +280,8 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   d.num_wires = C.num_wires; d.num_routed = C.num_routed; d.num_constants = C.num_constants; d.ngc = C.num_gate_consts;
   d.ngroups = (int)C.grp_start.size(); d.nls = C.nls; d.nlp = C.nlp; d.npp = C.npp; d.qdf = C.qdf; d.nluts = (int)C.lut_in.size();
   d.depth0 = C.depth0; d.final_len = C.final_len;
-  for (int t = 0; t < 4; t++) d.width[t] = C.oracle_width[t];
+  for (int t = 0; t < 4; t++) { d.width[t] = C.oracle_width[t]; d.lwidth[t] = C.leaf_width[t]; }
+  d.noop_leaves = C.noop_leaves ? 1 : 0;
   d.n_gates = C.n_gate_eval; d.n_pp_terms = (int)C.n_pp_terms_per_round; d.n_lookup_terms = (int)C.n_lookup_terms_per_round;
   d.alpha_base_gates = C.alpha_base_gates;
   const Layout& L = C.L;
@@ -261,7 +292,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   {   // unit orders: most expensive tree first (stable), see DevCircuit::leaf_order
     std::vector<std::pair<int64_t, int>> lc, mc;
     for (int t = 0; t < d.T; t++) {
-      const int64_t len = t < 4 ? C.oracle_width[t] : (2ll << C.arities[t - 4]);
+      const int64_t len = t < 4 ? C.leaf_width[t] : (2ll << C.arities[t - 4]);
       lc.push_back({-(len + 7) / 8, t});
       mc.push_back({-(int64_t)(t < 4 ? C.depth0 : C.step_depth[t - 4]), t});
     }
@@ -389,6 +420,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (e == hipSuccess) { for (auto& x : v->ev) { e = hipEventCreate(&x); if (e != hipSuccess) break; } v->timed = e == hipSuccess; }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_p1, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_side, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_tr, hipEventDisableTiming);
   // the side stream carries few, long-latency waves (vanishing items, FRI queries); a
   // high-priority queue for it was measured (P2V_SIDE_PRIO=1) and changed nothing
   if (e == hipSuccess) {
@@ -458,16 +490,31 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   else if (v->transcript_mode == 2) tl = 4;
   const int nt_blocks = (tl * d.B + 255) / 256;
   const int leaf_units = d.Q * d.T * NPB;
-  T0(1, st);
-  k_phase1<<<nt_blocks + (leaf_units + 3) / 4, 256, 0, st>>>(d, nt_blocks, tl);
-  DBG("k_phase1", st);
-  T1(1, st);
+  if (!v->split_phase1 || sd == st) {
+    T0(1, st);
+    k_phase1<<<nt_blocks + (leaf_units + 3) / 4, 256, 0, st>>>(d, nt_blocks, tl);
+    DBG("k_phase1", st);
+    T1(1, st);
+    if (sd != st) {
+      HCK(hipEventRecord(v->dep_p1, st));
+      HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));
+    }
+  } else {
+    HCK(hipEventRecord(v->dep_p1, st));   // the batch is ready on st (H2D, caller's stream order)
+    HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));
+    T0(9, sd);
+    k_transcript<<<nt_blocks, 256, 0, sd>>>(d, tl);
+    DBG("k_transcript", sd);
+    T1(9, sd);
+    HCK(hipEventRecord(v->dep_tr, sd));
+    T0(8, st);
+    k_leaf<<<(leaf_units + 3) / 4, 256, 0, st>>>(d);
+    DBG("k_leaf", st);
+    T1(8, st);
+    HCK(hipStreamWaitEvent(st, v->dep_tr, 0));   // k_merkle reads the query indices
+  }
   // phase 2: Merkle paths on the main stream; FRI queries and the vanishing kernel (few,
   // long-latency waves) on the side stream, concurrently
-  if (sd != st) {
-    HCK(hipEventRecord(v->dep_p1, st));
-    HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));
-  }
   T0(7, sd);
   if (d.n_lut_pieces > 0) k_lut<<<(d.r * d.n_lut_pieces * NPB + 3) / 4, 256, 0, sd>>>(d);
   DBG("k_lut", sd);

@@ -133,16 +133,32 @@ static void expand_strategy(Circuit& C, int tag, const std::vector<int64_t>& a) 
   } else if (tag == STRAT_FIXED) {
     for (int64_t x : a) C.arities.push_back((int)x);
   } else if (tag == STRAT_MIN_SIZE) {
+    if (a.size() > 1) throw ParseError("MinSize: expecting an optional max arity");
     throw CircuitError("reduction strategy not implemented (MinSize), Plonk/FRI.hs:342");
   } else {
     throw ParseError("FriReductionStrategy: unknown constructor tag");
   }
 }
 
+// The FRI steps: the reference expands the strategy (above); P2V_EXT_PARAMS_ARITIES takes
+// fri_params.reduction_arity_bits as plonky2's verifier does (any strategy, MinSize included;
+// the strategy is still decoded and its shape checked).
+static void fri_steps(Circuit& C, int tag, const std::vector<int64_t>& a) {
+  if (C.ext & P2V_EXT_PARAMS_ARITIES) {
+    if (tag == STRAT_CONSTANT_ARITY_BITS && a.size() != 2) throw ParseError("ConstantArityBits: expecting [arity_bits, final_poly_bits]");
+    if (tag == STRAT_MIN_SIZE && a.size() > 1) throw ParseError("MinSize: expecting an optional max arity");
+    if (tag < STRAT_FIXED || tag > STRAT_MIN_SIZE) throw ParseError("FriReductionStrategy: unknown constructor tag");
+    C.arities = C.params_arities;
+  } else {
+    expand_strategy(C, tag, a);
+  }
+}
+
 static void finalize_circuit(Circuit& C);
 
-Circuit parse_circuit(const JVal& common, const JVal& vkey) {
+Circuit parse_circuit(const JVal& common, const JVal& vkey, uint32_t ext) {
   Circuit C;
+  C.ext = ext;
   const JVal& cfg = common.at("config");
   C.num_wires = (int)j_int(cfg.at("num_wires"));
   C.num_routed = (int)j_int(cfg.at("num_routed_wires"));
@@ -161,21 +177,25 @@ Circuit parse_circuit(const JVal& common, const JVal& vkey) {
   const JVal& rs = fc.at("reduction_strategy");
   if (rs.kind != JVal::Obj || rs.keys.size() != 1) throw ParseError("reduction_strategy: expecting a singleton object");
   const JVal& fp = common.at("fri_params");
-  (void)j_bool(fp.at("hiding"));
+  C.hiding = j_bool(fp.at("hiding"));
   C.degree_bits = (int)j_int(fp.at("degree_bits"));
-  (void)fp.at("reduction_arity_bits").arr();
+  for (const auto& x : fp.at("reduction_arity_bits").arr()) C.params_arities.push_back((int)j_int(x));
   (void)fp.at("config");
   C.lde_bits = C.degree_bits + C.rate_bits;
   if (rs.keys[0] == "ConstantArityBits") {
     const auto& ab = rs.items[0].arr();
     if (ab.size() != 2) throw ParseError("ConstantArityBits: expecting [arity_bits, final_poly_bits]");
-    expand_strategy(C, STRAT_CONSTANT_ARITY_BITS, {j_int(ab[0]), j_int(ab[1])});
+    fri_steps(C, STRAT_CONSTANT_ARITY_BITS, {j_int(ab[0]), j_int(ab[1])});
   } else if (rs.keys[0] == "Fixed") {
     std::vector<int64_t> xs;
     for (const auto& x : rs.items[0].arr()) xs.push_back(j_int(x));
-    expand_strategy(C, STRAT_FIXED, xs);
-  } else if (rs.keys[0] == "MinSize") {
-    expand_strategy(C, STRAT_MIN_SIZE, {});
+    fri_steps(C, STRAT_FIXED, xs);
+  } else if (rs.keys[0] == "MinSize") {   // Maybe Log2: null or a number (Types.hs:131)
+    const JVal& mx = rs.items[0];
+    std::vector<int64_t> xs;
+    if (mx.kind == JVal::Num) xs.push_back(j_int(mx));
+    else if (mx.kind != JVal::Null) throw ParseError("MinSize: expecting null or an arity");
+    fri_steps(C, STRAT_MIN_SIZE, xs);
   } else {
     throw ParseError("FromJSON/FriReductionStrategy: unrecognized FRI reduction strategy");
   }
@@ -256,6 +276,11 @@ static void finalize_circuit(Circuit& C) {
   C.oracle_width[1] = C.num_wires;
   C.oracle_width[2] = C.r * (1 + C.npp + C.nlp);
   C.oracle_width[3] = C.r * C.qdf;
+  {
+    const int salt = (C.ext & P2V_EXT_HIDING) && C.hiding ? 4 : 0;   // SALT_SIZE; constants/sigmas are never salted
+    for (int t = 0; t < 4; t++) C.leaf_width[t] = C.oracle_width[t] + (t == 0 ? 0 : salt);
+  }
+  C.noop_leaves = (C.ext & P2V_EXT_HASH_OR_NOOP) != 0;
   C.depth0 = C.lde_bits - C.cap_height;
   if (C.depth0 < 0) throw CircuitError("cap_height exceeds the LDE size");
   { int logn = C.lde_bits; for (int a : C.arities) { logn -= a; C.step_depth.push_back(std::max(0, logn - C.cap_height)); } }
@@ -300,7 +325,7 @@ static void finalize_circuit(Circuit& C) {
   L.pow = w; w += 1;
   L.q0 = w;
   int64_t q = 0;
-  for (int t = 0; t < 4; t++) { L.leaf[t] = q; q += C.oracle_width[t]; }
+  for (int t = 0; t < 4; t++) { L.leaf[t] = q; q += C.leaf_width[t]; }
   for (int t = 0; t < 4; t++) { L.path[t] = q; q += 4 * C.depth0; }
   for (size_t s = 0; s < C.arities.size(); s++) {
     L.step_evals.push_back(q); q += 2 * (1 << C.arities[s]);
@@ -381,7 +406,7 @@ void pack_proof(const Circuit& C, const JVal& root, uint64_t* dst, int32_t* rec)
     for (int t = 0; t < 4; t++) {
       const auto& pair = ep[t].arr();
       if (pair.size() != 2) throw ParseError("evals_proofs entry must be a pair");
-      P.fields(pair[0], base + L.leaf[t], C.oracle_width[t], "initial tree leaf");
+      P.fields(pair[0], base + L.leaf[t], C.leaf_width[t], "initial tree leaf");
       P.digests(pair[1].at("siblings"), base + L.path[t], C.depth0, "initial tree siblings");
     }
     const auto& st = qr[q].at("steps").arr();
@@ -431,10 +456,11 @@ const char* gate_name(int k) {
 }
 }  // namespace
 
-Circuit parse_circuit_words(const uint64_t* w, size_t n) {
+Circuit parse_circuit_words(const uint64_t* w, size_t n, uint32_t ext) {
   WordReader R{w, n};
   R.magic(P2V_WORDS_CIRCUIT_MAGIC);
   Circuit C;
+  C.ext = ext;
   // CircuitConfig (Types.hs:73-84)
   C.num_wires = (int)R.s("config_num_wires");
   C.num_routed = (int)R.s("config_num_routed_wires");
@@ -450,11 +476,11 @@ Circuit parse_circuit_words(const uint64_t* w, size_t n) {
   read_fri_config(R, C.rate_bits, C.cap_height, C.pow_bits, tag, sargs, C.num_queries);
   // FriParams (Types.hs:151-157): its own FriConfig copy, hiding, degree_bits, arity bits
   read_fri_config(R, d0, d1, d2, tag2, sargs2, d3);
-  (void)R.b("fri_hiding");
+  C.hiding = R.b("fri_hiding");
   C.degree_bits = (int)R.s("fri_degree_bits");
-  for (int64_t k = R.len("fri_reduction_arity_bits"); k > 0; k--) (void)R.s("fri_reduction_arity_bits");
+  for (int64_t k = R.len("fri_reduction_arity_bits"); k > 0; k--) C.params_arities.push_back((int)R.s("fri_reduction_arity_bits"));
   C.lde_bits = C.degree_bits + C.rate_bits;
-  expand_strategy(C, tag, sargs);
+  fri_steps(C, tag, sargs);
   // gates (Gate/Base.hs:27-45)
   for (int64_t k = R.len("circuit_gates"); k > 0; k--) {
     GateDesc g;
@@ -558,7 +584,7 @@ void pack_proof_words(const Circuit& C, const uint64_t* w, size_t n, uint64_t* d
     const int64_t base = L.q0 + (int64_t)q * L.qstride;
     if (R.len("evals_proofs") != 4) throw ShapeError("checkInitialTreeProofs: expecting 4 Merkle proofs for the 4 oracles");
     for (int t = 0; t < 4; t++) {
-      fields(base + L.leaf[t], C.oracle_width[t], "initial tree leaf");
+      fields(base + L.leaf[t], C.leaf_width[t], "initial tree leaf");
       digests(base + L.path[t], C.depth0, "initial tree siblings");
     }
     if (R.len("steps") != S) throw ShapeError("steps: expected " + std::to_string(S));
@@ -571,6 +597,83 @@ void pack_proof_words(const Circuit& C, const uint64_t* w, size_t n, uint64_t* d
   dst[L.pow] = R.f("pow_witness");
   fields(L.pis, C.num_pis, "public_inputs");   // ProofWithPublicInputs: the_proof, public_inputs
   if (R.i != n) throw ParseError("words: trailing words after ProofWithPublicInputs");
+}
+
+// ------------------------------------------------------------------ plonky2 binary proofs
+// ProofWithPublicInputs in plonky2's own byte serialization (util/serialization: Write::
+// write_proof_with_public_inputs), the step before JSON in deployments (SURVEY.md §8f row 3;
+// unchecked in the reference, README.md:27).  Restated from plonky2 (not in /root/reference):
+// u64 little-endian words; F = its canonical u64 (reduced mod p here, as the JSON path reduces);
+// FExt = 2 F; HashOut = 4 F; MerkleCap = 2^cap_height hashes (no length); MerkleProof = u8
+// sibling count, then the hashes; vectors whose length the circuit fixes carry no length.
+//   Proof: wires_cap, plonk_zs_partial_products_cap, quotient_polys_cap,
+//     OpeningSet: constants, plonk_sigmas, wires, plonk_zs, plonk_zs_next, lookup_zs,
+//       lookup_zs_next, partial_products, quotient_polys,
+//     FriProof: commit-phase caps, query rounds (4 x (leaf [F], MerkleProof), steps x
+//       (evals [FExt], MerkleProof)), final_poly [FExt], pow_witness F
+//   public_inputs: the remaining words, or a u64 count then the words (both forms occur; the
+//     remaining byte count tells them apart).
+// Parity unpinned: no binary fixture exists offline; tests check it against the JSON path.
+namespace {
+struct ByteReader {
+  const uint8_t* b; size_t n; size_t i = 0;
+  uint64_t u64(const char* what) {
+    if (n - i < 8) throw ParseError(std::string("bytes: truncated at ") + what);
+    uint64_t x = 0;
+    for (int k = 7; k >= 0; k--) x = (x << 8) | b[i + k];
+    i += 8;
+    return x;
+  }
+  uint8_t u8(const char* what) { if (i >= n) throw ParseError(std::string("bytes: truncated at ") + what); return b[i++]; }
+};
+}  // namespace
+
+void pack_proof_bytes(const Circuit& C, const uint8_t* bytes, size_t n, uint64_t* dst) {
+  const Layout& L = C.L;
+  ByteReader R{bytes, n};
+  auto fields = [&](int64_t off, int64_t k, const char* what) { for (int64_t i = 0; i < k; i++) dst[off + i] = R.u64(what) % gl::P; };
+  auto exts = [&](int64_t off, int64_t k, const char* what) { fields(off, 2 * k, what); };
+  auto cap = [&](int64_t off, const char* what) { fields(off, 4 * (int64_t)C.cap_len, what); };
+  auto path = [&](int64_t off, int depth, const char* what) {
+    const int len = R.u8(what);
+    if (len != depth) throw ShapeError(std::string(what) + ": expected " + std::to_string(depth) + " siblings, got " + std::to_string(len));
+    fields(off, 4 * (int64_t)depth, what);
+  };
+  cap(L.wcap, "wires_cap");
+  cap(L.zcap, "plonk_zs_partial_products_cap");
+  cap(L.qcap, "quotient_polys_cap");
+  exts(L.o_const, C.num_constants, "openings.constants");
+  exts(L.o_sig, C.num_routed, "openings.plonk_sigmas");
+  exts(L.o_wires, C.num_wires, "openings.wires");
+  exts(L.o_zs, C.r, "openings.plonk_zs");
+  exts(L.o_zs_next, C.r, "openings.plonk_zs_next");
+  exts(L.o_lzs, (int64_t)C.r * C.nlp, "openings.lookup_zs");
+  exts(L.o_lzs_next, (int64_t)C.r * C.nlp, "openings.lookup_zs_next");
+  exts(L.o_pp, (int64_t)C.r * C.npp, "openings.partial_products");
+  exts(L.o_quot, (int64_t)C.r * C.qdf, "openings.quotient_polys");
+  const int S = (int)C.arities.size();
+  for (int s = 0; s < S; s++) cap(L.ccaps + (int64_t)s * 4 * C.cap_len, "commit_phase_merkle_caps");
+  for (int q = 0; q < C.num_queries; q++) {
+    const int64_t base = L.q0 + (int64_t)q * L.qstride;
+    for (int t = 0; t < 4; t++) {
+      fields(base + L.leaf[t], C.leaf_width[t], "initial tree leaf");
+      path(base + L.path[t], C.depth0, "initial tree siblings");
+    }
+    for (int s = 0; s < S; s++) {
+      exts(base + L.step_evals[s], 1 << C.arities[s], "step evals");
+      path(base + L.step_path[s], C.step_depth[s], "step siblings");
+    }
+  }
+  exts(L.final_poly, C.final_len, "final_poly.coeffs");
+  dst[L.pow] = R.u64("pow_witness") % gl::P;
+  const size_t rest = n - R.i, np = (size_t)C.num_pis;
+  if (rest == 8 * np) fields(L.pis, C.num_pis, "public_inputs");
+  else if (rest == 8 * (np + 1)) {
+    if (R.u64("public_inputs length") != np) throw ShapeError("public_inputs: length prefix differs from num_public_inputs");
+    fields(L.pis, C.num_pis, "public_inputs");
+  } else {
+    throw ShapeError("public_inputs: " + std::to_string(rest) + " trailing bytes for " + std::to_string(np) + " public inputs");
+  }
 }
 
 // ------------------------------------------------------------------ template-guided pack

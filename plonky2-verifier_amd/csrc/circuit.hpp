@@ -44,6 +44,9 @@ struct Circuit {
   // FriConfig / FriParams (Types.hs:116-174)
   int rate_bits = 0, cap_height = 0, pow_bits = 0, num_queries = 0, degree_bits = 0, lde_bits = 0;
   std::vector<int> arities;                 // expandReductionStrategy, Plonk/FRI.hs:337-354
+  bool hiding = false;                      // fri_params.hiding (Types.hs:153)
+  std::vector<int> params_arities;          // fri_params.reduction_arity_bits (Types.hs:155)
+  uint32_t ext = 0;                         // P2V_EXT_* (include/p2v.h): opt-in plonky2 conventions
   // CommonCircuitData (Types.hs:47-61)
   std::vector<GateDesc> gates;
   std::vector<int> sel_idx;
@@ -57,7 +60,9 @@ struct Circuit {
   uint64_t digest[4] = {0, 0, 0, 0};
   // derived
   int cap_len = 0, final_len = 0;
-  int oracle_width[4] = {0, 0, 0, 0};
+  int oracle_width[4] = {0, 0, 0, 0};       // data columns per initial oracle (Plonk/FRI.hs:56-65)
+  int leaf_width[4] = {0, 0, 0, 0};         // packed leaf words: + SALT_SIZE salts under P2V_EXT_HIDING
+  bool noop_leaves = false;                 // P2V_EXT_HASH_OR_NOOP: leaves of <= 4 words are their digest
   int depth0 = 0;                           // initial Merkle path length
   std::vector<int> step_depth;
   int n_gate_eval = 0;                      // gates actually evaluated: min(#selector_indices, #gates)
@@ -67,10 +72,12 @@ struct Circuit {
   int64_t trace_words = 0;
 };
 
-Circuit parse_circuit(const JVal& common, const JVal& vkey);   // throws ParseError / CircuitError
+Circuit parse_circuit(const JVal& common, const JVal& vkey, uint32_t ext = 0);   // throws ParseError / CircuitError
 // the same from the word-encoded Types.hs values (include/p2v.h, "Word-encoded values")
-Circuit parse_circuit_words(const uint64_t* words, size_t n);   // throws ParseError / CircuitError
+Circuit parse_circuit_words(const uint64_t* words, size_t n, uint32_t ext = 0);   // throws ParseError / CircuitError
 void pack_proof_words(const Circuit& c, const uint64_t* words, size_t n, uint64_t* dst);   // ParseError / ShapeError
+// plonky2's binary ProofWithPublicInputs serialization (circuit.cpp); ParseError / ShapeError
+void pack_proof_bytes(const Circuit& c, const uint8_t* bytes, size_t n, uint64_t* dst);
 // throws ParseError / ShapeError; rec (optional, [words]) receives each packed word's number ordinal
 void pack_proof(const Circuit& c, const JVal& proof, uint64_t* dst, int32_t* rec = nullptr);
 

@@ -17,7 +17,9 @@ struct DevCircuit {
   int32_t num_wires, num_routed, num_constants, ngc, ngroups, nls, nlp, npp, qdf, nluts;
   int32_t depth0, final_len;
   int32_t arity[P2V_MAX_STEPS], step_depth[P2V_MAX_STEPS], step_logn[P2V_MAX_STEPS];
-  int32_t width[4];
+  int32_t width[4];                // data columns per initial oracle (combineInitial)
+  int32_t lwidth[4];               // packed leaf words (width + salts under P2V_EXT_HIDING): the sponged row
+  int32_t noop_leaves;             // P2V_EXT_HASH_OR_NOOP: a leaf of <= 4 words is its own digest
   // tree t of each unit position, most expensive first, so long waves dispatch first and short
   // ones fill the tail: leaf hashing by sponge length, Merkle paths by depth
   int8_t leaf_order[4 + P2V_MAX_STEPS], merkle_order[4 + P2V_MAX_STEPS];

@@ -66,6 +66,12 @@ void sponge(const u64* xs, size_t n, u64 out[4]) {
   }
   memcpy(out, st, 32);
 }
+// a Merkle leaf's digest: the sponge (Hash/Merkle.hs:27-28), or under the hash_or_noop
+// extension (P2V_EXT_HASH_OR_NOOP) a leaf of <= 4 elements zero-padded (plonky2 hash_or_noop)
+void leaf_digest(const u64* xs, size_t n, bool noop, u64 out[4]) {
+  if (noop && n <= 4) { memset(out, 0, 32); memcpy(out, xs, n * 8); return; }
+  sponge(xs, n, out);
+}
 void compress(const u64* a, const u64* b, u64 out[4]) {
   u64 st[12] = {0};
   memcpy(st, a, 32); memcpy(st + 4, b, 32);
@@ -191,6 +197,11 @@ struct J {
 struct Circuit {
   int degree_bits = 12, rate_bits = 3, cap_height = 4, pow_bits = 16, num_queries = 28;
   int arity_bits = 4, final_poly_bits = 5;
+  // opt-in plonky2 conventions (include/p2v.h P2V_EXT_*): 1 the steps are `arity_seq` written as
+  // fri_params.reduction_arity_bits under a MinSize strategy; 2 hiding (4 salts per wires / zs /
+  // quotient leaf); 4 hash_or_noop leaves.  arity_seq without bit 1: a Fixed strategy.
+  unsigned ext = 0;
+  std::vector<int> arity_seq;
   int num_wires = 135, num_routed = 80, num_gate_consts = 2, r = 2, qdf = 8;
   int num_pis = 4;
   int ngroups = 3;
@@ -441,7 +452,9 @@ void build_circuit(Circuit& C) {
   C.num_constants = C.ngroups + C.nls + C.num_gate_consts;
   C.npp = (C.num_routed + C.qdf - 1) / C.qdf - 1;
   C.arities.clear();
-  for (int logn = C.degree_bits; logn > C.final_poly_bits; logn -= C.arity_bits) C.arities.push_back(C.arity_bits);
+  if (!C.arity_seq.empty()) C.arities = C.arity_seq;
+  else for (int logn = C.degree_bits; logn > C.final_poly_bits; logn -= C.arity_bits) C.arities.push_back(C.arity_bits);
+  { int sa = 0; for (int a : C.arities) sa += a; if (sa > C.degree_bits) throw std::runtime_error("gen: FRI arities fold below degree 1"); }
   C.k_is.resize(C.num_routed);
   { u64 k = 1; for (int i = 0; i < C.num_routed; i++) { C.k_is[i] = k; k = gl::mul(k, gl::MULT_GEN); } }
   size_t M = (size_t)1 << C.lde_bits;
@@ -513,7 +526,7 @@ void build_circuit(Circuit& C) {
     }
   }
   std::vector<Digest> leaves(M);
-  for (size_t idx = 0; idx < M; idx++) sponge(&C.const_lde[idx * C.const_width], C.const_width, leaves[idx].e);
+  for (size_t idx = 0; idx < M; idx++) leaf_digest(&C.const_lde[idx * C.const_width], C.const_width, C.ext & 4, leaves[idx].e);
   C.const_tree.build(std::move(leaves), C.lde_bits, C.cap_height);
 
   // ---------------------------------------------------------- JSON (Types.hs field names)
@@ -521,14 +534,19 @@ void build_circuit(Circuit& C) {
   auto fri_config = [&](J& o) {
     o.raw("{\"rate_bits\":"); o.i(C.rate_bits); o.raw(",\"cap_height\":"); o.i(C.cap_height);
     o.raw(",\"proof_of_work_bits\":"); o.i(C.pow_bits);
-    o.raw(",\"reduction_strategy\":{\"ConstantArityBits\":["); o.i(C.arity_bits); o.raw(","); o.i(C.final_poly_bits); o.raw("]}");
+    if (C.ext & 1) o.raw(",\"reduction_strategy\":{\"MinSize\":null}");
+    else if (!C.arity_seq.empty()) {
+      o.raw(",\"reduction_strategy\":{\"Fixed\":[");
+      for (size_t k = 0; k < C.arity_seq.size(); k++) { if (k) o.raw(","); o.i(C.arity_seq[k]); }
+      o.raw("]}");
+    } else { o.raw(",\"reduction_strategy\":{\"ConstantArityBits\":["); o.i(C.arity_bits); o.raw(","); o.i(C.final_poly_bits); o.raw("]}"); }
     o.raw(",\"num_query_rounds\":"); o.i(C.num_queries); o.raw("}");
   };
   j.raw("{\"config\":{\"num_wires\":"); j.i(C.num_wires); j.raw(",\"num_routed_wires\":"); j.i(C.num_routed);
   j.raw(",\"num_constants\":"); j.i(C.num_gate_consts); j.raw(",\"use_base_arithmetic_gate\":true,\"security_bits\":100");
-  j.raw(",\"num_challenges\":"); j.i(C.r); j.raw(",\"zero_knowledge\":false,\"randomize_unused_wires\":true");
+  j.raw(",\"num_challenges\":"); j.i(C.r); j.raw((C.ext & 2) ? ",\"zero_knowledge\":true" : ",\"zero_knowledge\":false"); j.raw(",\"randomize_unused_wires\":true");
   j.raw(",\"max_quotient_degree_factor\":"); j.i(C.qdf); j.raw(",\"fri_config\":"); fri_config(j); j.raw("}");
-  j.raw(",\"fri_params\":{\"config\":"); fri_config(j); j.raw(",\"hiding\":false,\"degree_bits\":"); j.i(C.degree_bits);
+  j.raw(",\"fri_params\":{\"config\":"); fri_config(j); j.raw((C.ext & 2) ? ",\"hiding\":true" : ",\"hiding\":false"); j.raw(",\"degree_bits\":"); j.i(C.degree_bits);
   j.raw(",\"reduction_arity_bits\":["); for (size_t k = 0; k < C.arities.size(); k++) { if (k) j.raw(","); j.i(C.arities[k]); } j.raw("]}");
   j.raw(",\"gates\":[");
   for (size_t g = 0; g < C.gates.size(); g++) { if (g) j.raw(","); j.raw("\""); j.raw(C.gates[g].c_str()); j.raw("\""); }
@@ -570,17 +588,34 @@ struct Witness {
   std::vector<u64> q_lde;                        // [M][r*qdf] (all zero)
   int zw = 0, qw = 0;
   Tree wires_tree, zs_tree, q_tree;
+  std::vector<u64> salt[3];                      // hiding: [M][4] salts of the wires / zs / quotient leaves
   // real mode
   std::vector<u64> pis;                          // public inputs (fixed by the witness: PublicInputGate)
   std::vector<std::vector<u64>> zs_coeffs;       // [r*(1+npp)] Z_j, then the partial products
   std::vector<std::vector<u64>> q_coeffs;        // [r*qdf] quotient chunks
 };
 
-void tree_of_rows(const std::vector<u64>& rows, int width, int lde_bits, int cap_height, Tree& t) {
+// the leaf row of position idx: the oracle's row, then its salts (hiding), as the proof carries it
+void leaf_row(const u64* row, int width, const std::vector<u64>& salt, size_t idx, std::vector<u64>& out) {
+  out.assign(row, row + width);
+  if (!salt.empty()) out.insert(out.end(), salt.begin() + idx * 4, salt.begin() + idx * 4 + 4);
+}
+void tree_of_rows(const std::vector<u64>& rows, int width, int lde_bits, int cap_height, Tree& t,
+                  const std::vector<u64>& salt = {}, bool noop = false) {
   const size_t M = (size_t)1 << lde_bits;
   std::vector<Digest> leaves(M);
-  parallel_for(M, [&](size_t idx) { sponge(&rows[idx * width], width, leaves[idx].e); });
+  parallel_for(M, [&](size_t idx) {
+    std::vector<u64> lr;
+    leaf_row(&rows[idx * width], width, salt, idx, lr);
+    leaf_digest(lr.data(), lr.size(), noop, leaves[idx].e);
+  });
   t.build(std::move(leaves), lde_bits, cap_height);
+}
+void make_salts(const Circuit& C, Witness* W, u64 seed) {
+  if (!(C.ext & 2)) return;
+  Rng rg(seed * 31337 + 7);
+  const size_t M = (size_t)1 << C.lde_bits;
+  for (auto& s : W->salt) { s.resize(M * 4); for (auto& x : s) x = rg.field(); }
 }
 
 void batch_inv_base(std::vector<u64>& v) {   // Montgomery's trick over F (no zeros expected)
@@ -599,6 +634,7 @@ void batch_inv_base(std::vector<u64>& v) {   // Montgomery's trick over F (no ze
 Witness* make_witness_real(const Circuit& C, u64 seed) {
   auto* W = new Witness();
   Rng rg(seed * 1000003 + 11);
+  make_salts(C, W, seed);
   const int N = C.N, NW = C.num_wires, NR = C.num_routed, NK = C.num_gate_consts, r = C.r, n = C.degree_bits;
   W->pis.resize(C.num_pis);
   for (auto& x : W->pis) x = rg.field();
@@ -632,7 +668,7 @@ Witness* make_witness_real(const Circuit& C, u64 seed) {
     W->wire_coeffs[c] = interpolate(std::move(v), n);
   });
   W->wires_lde = oracle_rows(W->wire_coeffs, C.lde_bits);
-  tree_of_rows(W->wires_lde, NW, C.lde_bits, C.cap_height, W->wires_tree);
+  tree_of_rows(W->wires_lde, NW, C.lde_bits, C.cap_height, W->wires_tree, W->salt[0], C.ext & 4);
   Duplex d;
   for (int i = 0; i < 4; i++) d.absorb(C.circuit_digest.e[i]);
   for (int i = 0; i < 4; i++) d.absorb(pih[i]);
@@ -675,7 +711,7 @@ Witness* make_witness_real(const Circuit& C, u64 seed) {
   W->zs_coeffs.resize(W->zw);
   parallel_for(W->zw, [&](size_t c) { W->zs_coeffs[c] = interpolate(zcols[c], n); });
   W->zs_lde = oracle_rows(W->zs_coeffs, C.lde_bits);
-  tree_of_rows(W->zs_lde, W->zw, C.lde_bits, C.cap_height, W->zs_tree);
+  tree_of_rows(W->zs_lde, W->zw, C.lde_bits, C.cap_height, W->zs_tree, W->salt[1], C.ext & 4);
   d.absorb_digests(W->zs_tree.cap());
   for (auto& a : alphas) a = d.squeeze();
   // ---- the quotient: C_i(x) / (x^n - 1) on g<nu>, |<nu>| = 2^q_bits >= (qdf + 1) n
@@ -738,13 +774,14 @@ Witness* make_witness_real(const Circuit& C, u64 seed) {
     }
   }
   W->q_lde = oracle_rows(W->q_coeffs, C.lde_bits);
-  tree_of_rows(W->q_lde, W->qw, C.lde_bits, C.cap_height, W->q_tree);
+  tree_of_rows(W->q_lde, W->qw, C.lde_bits, C.cap_height, W->q_tree, W->salt[2], C.ext & 4);
   return W;
 }
 
 Witness* make_witness(const Circuit& C, u64 seed) {
   auto* W = new Witness();
   Rng rg(seed * 1000003 + 11);
+  make_salts(C, W, seed);
   size_t M = (size_t)1 << C.lde_bits;
   W->wire_coeffs.assign(C.num_wires, std::vector<u64>(C.N));
   for (auto& p : W->wire_coeffs) for (auto& c : p) c = rg.field();
@@ -766,14 +803,9 @@ Witness* make_witness(const Circuit& C, u64 seed) {
   }
   W->qw = C.r * C.qdf;
   W->q_lde.assign(M * W->qw, 0);
-  auto tree_of = [&](const std::vector<u64>& rows, int width, Tree& t) {
-    std::vector<Digest> leaves(M);
-    for (size_t idx = 0; idx < M; idx++) sponge(&rows[idx * width], width, leaves[idx].e);
-    t.build(std::move(leaves), C.lde_bits, C.cap_height);
-  };
-  tree_of(W->wires_lde, C.num_wires, W->wires_tree);
-  tree_of(W->zs_lde, W->zw, W->zs_tree);
-  tree_of(W->q_lde, W->qw, W->q_tree);
+  tree_of_rows(W->wires_lde, C.num_wires, C.lde_bits, C.cap_height, W->wires_tree, W->salt[0], C.ext & 4);
+  tree_of_rows(W->zs_lde, W->zw, C.lde_bits, C.cap_height, W->zs_tree, W->salt[1], C.ext & 4);
+  tree_of_rows(W->q_lde, W->qw, C.lde_bits, C.cap_height, W->q_tree, W->salt[2], C.ext & 4);
   return W;
 }
 
@@ -889,7 +921,7 @@ std::string make_proof(const Circuit& C, const Witness& W, u64 pi_seed, unsigned
     std::vector<u64> flat(2 * ar);
     for (size_t jj = 0; jj < nl; jj++) {
       for (int k = 0; k < ar; k++) { flat[2 * k] = v[jj * ar + k].a; flat[2 * k + 1] = v[jj * ar + k].b; }
-      sponge(flat.data(), flat.size(), leaves[jj].e);
+      leaf_digest(flat.data(), flat.size(), C.ext & 4, leaves[jj].e);
     }
     Tree t; t.build(std::move(leaves), logn - ab, C.cap_height);
     d.absorb_digests(t.cap());
@@ -925,7 +957,8 @@ std::string make_proof(const Circuit& C, const Witness& W, u64 pi_seed, unsigned
   for (size_t i = 0; i < nf; i++) nat[gl::rev_bits(logn, (uint32_t)i)] = fin[i];
   efft(nat, logn, gl::inv(gl::subgroup_gen(logn)));
   u64 inv_nf = gl::inv((u64)nf), sinv = gl::inv(shift), sp = 1;
-  size_t final_len = (size_t)1 << (C.degree_bits - (int)C.arities.size() * C.arity_bits);
+  int sum_a = 0; for (int a : C.arities) sum_a += a;
+  size_t final_len = (size_t)1 << (C.degree_bits - sum_a);
   std::vector<E> final_poly(final_len);
   for (size_t k = 0; k < nf; k++) {
     E ck = gl::escale(gl::mul(inv_nf, sp), nat[k]);
@@ -963,14 +996,16 @@ std::string make_proof(const Circuit& C, const Witness& W, u64 pi_seed, unsigned
     if (q) j.raw(",");
     size_t idx = qidx[q];
     j.raw("{\"initial_trees_proof\":{\"evals_proofs\":[");
-    auto emit = [&](const u64* rowp, int width, const Tree& t, bool comma) {
+    std::vector<u64> lr;
+    auto emit = [&](const u64* rowp, int width, const Tree& t, const std::vector<u64>& salt, bool comma) {
       if (comma) j.raw(",");
-      j.raw("["); j.fs(rowp, width); j.raw(",{\"siblings\":"); j.cap(t.path(idx)); j.raw("}]");
+      leaf_row(rowp, width, salt, idx, lr);
+      j.raw("["); j.fs(lr.data(), lr.size()); j.raw(",{\"siblings\":"); j.cap(t.path(idx)); j.raw("}]");
     };
-    emit(&C.const_lde[idx * C.const_width], C.const_width, C.const_tree, false);
-    emit(&W.wires_lde[idx * C.num_wires], C.num_wires, W.wires_tree, true);
-    emit(&W.zs_lde[idx * W.zw], W.zw, W.zs_tree, true);
-    emit(&W.q_lde[idx * W.qw], W.qw, W.q_tree, true);
+    emit(&C.const_lde[idx * C.const_width], C.const_width, C.const_tree, {}, false);
+    emit(&W.wires_lde[idx * C.num_wires], C.num_wires, W.wires_tree, W.salt[0], true);
+    emit(&W.zs_lde[idx * W.zw], W.zw, W.zs_tree, W.salt[1], true);
+    emit(&W.q_lde[idx * W.qw], W.qw, W.q_tree, W.salt[2], true);
     j.raw("]},\"steps\":[");
     size_t qi = idx;
     for (size_t s = 0; s < step_trees.size(); s++) {
@@ -1001,11 +1036,15 @@ extern "C" {
 //         (1: the column is NoopGate's index); mode 1: a real circuit over the recursion gate
 //         set; mode 2: a real circuit over a small gate set (Noop, Constant, PublicInput,
 //         Arithmetic) that fits one selector group.  Real modes choose their own groups.
-void* p2v_gen_circuit_new2(int degree_bits, int num_pis, int lookups, uint64_t circuit_seed, int num_queries, int pow_bits,
-                           int ngroups, int mode) {
+// ext / arities (narities > 0): the opt-in plonky2 conventions of the Circuit fields above
+void* p2v_gen_circuit_new3(int degree_bits, int num_pis, int lookups, uint64_t circuit_seed, int num_queries, int pow_bits,
+                           int ngroups, int mode, unsigned ext, const int* arities, int narities) {
   try {
     auto* C = new Circuit();
     C->degree_bits = degree_bits; C->num_pis = num_pis; C->circuit_seed = circuit_seed;
+    C->ext = ext;
+    if ((ext & 1) && narities <= 0) throw std::runtime_error("gen: the MinSize form needs the arity list");
+    for (int k = 0; k < narities; k++) C->arity_seq.push_back(arities[k]);
     if (ngroups > 0) C->ngroups = ngroups;
     C->real = mode != 0; C->gate_set = mode == 2 ? 1 : 0;
     if (num_queries > 0) C->num_queries = num_queries;
@@ -1023,6 +1062,10 @@ void* p2v_gen_circuit_new2(int degree_bits, int num_pis, int lookups, uint64_t c
     build_circuit(*C);
     return C;
   } catch (std::exception& e) { g_err = e.what(); return nullptr; }
+}
+void* p2v_gen_circuit_new2(int degree_bits, int num_pis, int lookups, uint64_t circuit_seed, int num_queries, int pow_bits,
+                           int ngroups, int mode) {
+  return p2v_gen_circuit_new3(degree_bits, num_pis, lookups, circuit_seed, num_queries, pow_bits, ngroups, mode, 0, nullptr, 0);
 }
 void* p2v_gen_circuit_new(int degree_bits, int num_pis, int lookups, uint64_t circuit_seed, int num_queries, int pow_bits) {
   return p2v_gen_circuit_new2(degree_bits, num_pis, lookups, circuit_seed, num_queries, pow_bits, 0, 0);

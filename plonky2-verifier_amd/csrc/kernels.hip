@@ -1,12 +1,12 @@
 // kernels.hip — gfx950 kernels of the batch verifier (everything except the vanishing /
 // gate-constraint kernel, which lives in vanish.hip).
 //
-// Data layout: the packed proofs are transposed once into SoA ([word][B], B = batch padded
-// to 64), so in every kernel lane i of a wave handles proof (64*pb + i) and all other
-// indices (query, tree, step, word) are wave-uniform: loads are fully coalesced 512-B rows,
-// control flow never diverges, and the Poseidon round constants are scalar operands.
+// Data layout: the caller's proof-major batch ([n][words]) is read in place (devcommon.h ld();
+// P2V_PROOF_MAJOR=0 builds the older transposed [word][B] form).  In every kernel lane i of a
+// wave handles proof (64*pb + i) and all other indices (query, tree, step, word) are
+// wave-uniform: control flow never diverges and the Poseidon round constants are scalar operands.
 //
-//   k_transpose   proof-major -> SoA
+//   k_transpose   proof-major -> SoA (P2V_PROOF_MAJOR=0 only)
 //   k_phase1      transcript waves (a row or quad of lanes per proof, ~115 sequential permutations,
 //                 Challenge/Verifier.hs:58-103 + Challenge/FRI.hs:65-104) run in the SAME
 //                 launch as the leaf-hash waves (one lane per (proof, query, tree) sponge,
@@ -49,20 +49,37 @@ __device__ __forceinline__ void leaf_hash_unit(const DevCircuit& c, int unit, in
   const int p = pb * 64 + lane;
   const int64_t base = c.q0 + (int64_t)q * c.qstride;
   int64_t off; int len;
-  if (t < 4) { off = base + c.leaf[t]; len = c.width[t]; }
+  if (t < 4) { off = base + c.leaf[t]; len = c.lwidth[t]; }
   else { int s = t - 4; off = base + c.step_evals[s]; len = 2 << c.arity[s]; }
   uint64_t st[12];
 #pragma unroll
   for (int i = 0; i < 12; i++) st[i] = 0;
-  for (int i = 0; i < len; i += 8) {   // sponge, overwrite mode, no padding
+  if (c.noop_leaves && len <= 4) {   // P2V_EXT_HASH_OR_NOOP: plonky2 hash_or_noop, the leaf zero-padded
+#pragma unroll
+    for (int j = 0; j < 4; j++) if (j < len) st[j] = ld(c, off + j, p);
+    len = 0;
+  }
+  // sponge, overwrite mode, no padding.  Two 8-word blocks per trip, both loaded up front: each
+  // lane streams its own proof's row, so the loads of one trip cover a whole 128-B line while
+  // it is resident in L2 (one block per load left half of every line to be fetched again after
+  // the permutation, profiles/r02_fetch_calibration.json)
+  for (int i = 0; i < len; i += 16) {
     const int k = len - i;
+    uint64_t nb[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) if (j < k) st[j] = ld(c, off + i + j, p);
+#pragma unroll
+    for (int j = 0; j < 8; j++) nb[j] = 8 + j < k ? ld(c, off + i + 8 + j, p) : 0;
     // words the rest of the sponge reads: the digest (0..3) after the last block, else the
     // words the next block does not overwrite (nx.. 11); state words 8..11 are 0 in block 0
-    const int nx = k - 8;
-    const int gm = nx <= 0 ? 1 : (nx >= 8 ? 4 : ((7 << (nx >> 2)) & 7));
-    p2::permute_dev(st, i == 0, gm);
+    int nx = k - 8;
+    p2::permute_dev(st, i == 0, nx <= 0 ? 1 : (nx >= 8 ? 4 : ((7 << (nx >> 2)) & 7)));
+    if (k > 8) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) if (8 + j < k) st[j] = nb[j];
+      nx = k - 16;
+      p2::permute_dev(st, false, nx <= 0 ? 1 : (nx >= 8 ? 4 : ((7 << (nx >> 2)) & 7)));
+    }
   }
   uint64_t* dst = c.leafdig + ((int64_t)(q * c.T + t) * 4) * c.B + p;
 #pragma unroll
@@ -278,6 +295,26 @@ extern "C" __global__ void __launch_bounds__(256) k_phase1(DevCircuit c, int nt_
   if (unit < units) leaf_hash_unit(c, unit, lane);
 }
 
+// The same two halves as separate launches (env P2V_PHASE1=split, api.cpp): on their own the leaf
+// waves run at the permutation's 72 VGPRs (7 waves/SIMD) instead of inheriting the transcript's
+// 123 (4 waves/SIMD), the transcript on the side stream beside them.  Measured slower (serial
+// 0.94x): the transcript chains then stretch to the leaf kernel's length; kept for measurement.
+extern "C" __global__ void __launch_bounds__(256) k_transcript(DevCircuit c, int tl) {
+  __builtin_amdgcn_s_setprio(3);
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (tl == 16) {
+    rp::Row R;
+    rp::init(R, threadIdx.x);
+    if ((g >> 4) < c.B) transcript_row(c, g >> 4, R);
+  } else {
+    if ((g >> 2) < c.B) transcript_quad(c, g >> 2, g & 3);
+  }
+}
+extern "C" __global__ void __launch_bounds__(256) k_leaf(DevCircuit c) {
+  const int unit = (int)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (unit < c.Q * c.T * (c.B >> 6)) leaf_hash_unit(c, unit, threadIdx.x & 63);
+}
+
 // ------------------------------------------------------------------------ Merkle paths
 extern "C" __global__ void __launch_bounds__(256) k_merkle(DevCircuit c) {
   const int lane = threadIdx.x & 63;
@@ -301,6 +338,8 @@ extern "C" __global__ void __launch_bounds__(256) k_merkle(DevCircuit c) {
   uint64_t cur[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) cur[i] = src[(int64_t)i * c.B];
+  // one level's 32 B of siblings per load: loading two levels at once (82 VGPRs) would cost a
+  // wave per SIMD (6 -> 5); the line re-fetches this leaves are served by the Infinity Cache
   for (int l = 0; l < depth; l++) {   // even index: compress(cur, sib), odd: compress(sib, cur)
     uint64_t sib[4];
 #pragma unroll

@@ -54,6 +54,8 @@ STATUS_MESSAGES = {
 
 # function return codes
 E_OK, E_PARSE, E_CIRCUIT, E_SHAPE, E_ARG, E_DEVICE, E_NODEVICE = 0, -1, -2, -3, -4, -5, -6
+# opt-in plonky2 conventions the reference does not implement (include/p2v.h P2V_EXT_*)
+EXT_PARAMS_ARITIES, EXT_HIDING, EXT_HASH_OR_NOOP, EXT_PLONKY2 = 1, 2, 4, 7
 
 FLAG_INPUT_DEVICE = 1
 FLAG_RESULT_DEVICE = 2
@@ -85,7 +87,7 @@ class _Info(ctypes.Structure):
         ("final_poly_len", ctypes.c_int32), ("num_public_inputs", ctypes.c_int32), ("num_openings_this", ctypes.c_int32),
         ("num_openings_next", ctypes.c_int32), ("has_lookups", ctypes.c_int32), ("num_gates", ctypes.c_int32),
         ("proof_words", ctypes.c_int64), ("trace_words", ctypes.c_int64), ("oracle_widths", ctypes.c_int32 * 4),
-        ("step_arity_bits", ctypes.c_int32 * 8),
+        ("step_arity_bits", ctypes.c_int32 * 8), ("leaf_widths", ctypes.c_int32 * 4), ("ext", ctypes.c_uint32),
     ]
 
 
@@ -108,7 +110,10 @@ def lib() -> ctypes.CDLL:
     L.p2v_pack_proof_json.argtypes = [vp, ctypes.c_char_p, sz, u64p]
     L.p2v_pack_proofs_json.argtypes = [vp, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz), sz, u64p, vp, ctypes.c_int]
     L.p2v_circuit_from_words.argtypes = [u64p, sz, ctypes.POINTER(vp)]
+    L.p2v_circuit_from_json_ex.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, sz, ctypes.c_uint32, ctypes.POINTER(vp)]
+    L.p2v_circuit_from_words_ex.argtypes = [u64p, sz, ctypes.c_uint32, ctypes.POINTER(vp)]
     L.p2v_pack_proof_words.argtypes = [vp, u64p, sz, u64p]
+    L.p2v_pack_proof_bytes.argtypes = [vp, ctypes.c_char_p, sz, u64p]
     L.p2v_device_count.argtypes = []
     L.p2v_verifier_create.argtypes = [vp, ctypes.c_int, sz, ctypes.POINTER(vp)]
     L.p2v_verifier_free.argtypes = [vp]
@@ -154,6 +159,8 @@ class CircuitInfo:
     trace_words: int
     oracle_widths: tuple
     step_arity_bits: tuple
+    leaf_widths: tuple = ()
+    ext: int = 0
 
 
 class VerifierCircuitData:
@@ -169,21 +176,24 @@ class VerifierCircuitData:
         self.info = CircuitInfo(
             inf.degree_bits, inf.lde_bits, inf.cap_height, inf.num_challenges, inf.num_query_rounds, inf.num_fri_steps,
             inf.final_poly_len, inf.num_public_inputs, inf.num_openings_this, inf.num_openings_next, bool(inf.has_lookups),
-            inf.num_gates, inf.proof_words, inf.trace_words, tuple(inf.oracle_widths), tuple(inf.step_arity_bits[: inf.num_fri_steps]))
+            inf.num_gates, inf.proof_words, inf.trace_words, tuple(inf.oracle_widths), tuple(inf.step_arity_bits[: inf.num_fri_steps]),
+            tuple(inf.leaf_widths), inf.ext)
 
     @classmethod
-    def from_json(cls, common_json: Union[str, bytes], vkey_json: Union[str, bytes]) -> "VerifierCircuitData":
+    def from_json(cls, common_json: Union[str, bytes], vkey_json: Union[str, bytes], ext: int = 0) -> "VerifierCircuitData":
+        """ext: opt-in plonky2 conventions the reference lacks (EXT_* below, include/p2v.h);
+        0 = exactly the reference's semantics."""
         c, v = _bytes(common_json), _bytes(vkey_json)
         h = ctypes.c_void_p()
-        _check(lib().p2v_circuit_from_json(c, len(c), v, len(v), ctypes.byref(h)))
+        _check(lib().p2v_circuit_from_json_ex(c, len(c), v, len(v), ext, ctypes.byref(h)))
         return cls(h.value)
 
     @classmethod
-    def from_words(cls, words: np.ndarray) -> "VerifierCircuitData":
+    def from_words(cls, words: np.ndarray, ext: int = 0) -> "VerifierCircuitData":
         """The word-encoded Types.hs value (include/p2v.h; what the Haskell shim marshals)."""
         w = np.ascontiguousarray(words, dtype=np.uint64)
         h = ctypes.c_void_p()
-        _check(lib().p2v_circuit_from_words(w.ctypes.data, w.size, ctypes.byref(h)))
+        _check(lib().p2v_circuit_from_words_ex(w.ctypes.data, w.size, ext, ctypes.byref(h)))
         return cls(h.value)
 
     @property
@@ -197,6 +207,16 @@ class VerifierCircuitData:
             out = np.empty(self.info.proof_words, dtype=np.uint64)
         assert out.dtype == np.uint64 and out.size == self.info.proof_words and out.flags.c_contiguous
         _check(lib().p2v_pack_proof_words(self._h, w.ctypes.data, w.size, out.ctypes.data))
+        return out
+
+    def pack_bytes(self, data: bytes, out: Optional[np.ndarray] = None) -> np.ndarray:
+        """plonky2's binary ProofWithPublicInputs serialization (include/p2v.h
+        p2v_pack_proof_bytes) -> packed u64 words of this circuit."""
+        b = bytes(data)
+        if out is None:
+            out = np.empty(self.info.proof_words, dtype=np.uint64)
+        assert out.dtype == np.uint64 and out.size == self.info.proof_words and out.flags.c_contiguous
+        _check(lib().p2v_pack_proof_bytes(self._h, b, len(b), out.ctypes.data))
         return out
 
     def pack(self, proof_json: Union[str, bytes], out: Optional[np.ndarray] = None) -> np.ndarray:

@@ -63,12 +63,15 @@ class Oracle:
         L.or_gate_kind.argtypes = [ctypes.c_char_p]
         L.or_verify_many.argtypes = [vp, ctypes.POINTER(vp), ctypes.c_long, vp, ctypes.c_int]
         L.or_verify_many.restype = ctypes.c_long
+        L.or_circuit_set_ext.argtypes = [vp, ctypes.c_uint]
         self.L = L
 
-    def circuit(self, common: bytes, vkey: bytes):
+    def circuit(self, common: bytes, vkey: bytes, ext: int = 0):
+        """ext: the P2V_EXT_* conventions (include/p2v.h), 0 = the reference's."""
         h = self.L.or_circuit_load(common, len(common), vkey, len(vkey))
         if not h:
             raise ValueError(self.L.or_last_error().decode())
+        self.L.or_circuit_set_ext(h, ext)
         return h
 
     def proof(self, text: bytes):
@@ -85,8 +88,8 @@ class Oracle:
             return st, tr
         return self.L.or_verify(circ, proof, None, 0)
 
-    def verify_json(self, common: bytes, vkey: bytes, proof: bytes, trace=False, unit_filters=False):
-        c = self.circuit(common, vkey)
+    def verify_json(self, common: bytes, vkey: bytes, proof: bytes, trace=False, unit_filters=False, ext=0):
+        c = self.circuit(common, vkey, ext)
         p = self.proof(proof)
         try:
             return self.verify(c, p, trace=trace, unit_filters=unit_filters)
@@ -118,6 +121,9 @@ class Generator:
         L.p2v_gen_circuit_new2.restype = vp
         L.p2v_gen_circuit_new2.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_int]
+        L.p2v_gen_circuit_new3.restype = vp
+        L.p2v_gen_circuit_new3.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_uint, vp, ctypes.c_int]
         L.p2v_gen_common_json.restype = ctypes.c_char_p
         L.p2v_gen_common_json.argtypes = [vp]
         L.p2v_gen_vkey_json.restype = ctypes.c_char_p
@@ -136,11 +142,14 @@ class Generator:
         L.p2v_gen_last_error.restype = ctypes.c_char_p
         self.L = L
 
-    def circuit(self, degree_bits=12, num_pis=4, lookups=0, seed=1, queries=28, pow_bits=16, ngroups=0, mode=0):
+    def circuit(self, degree_bits=12, num_pis=4, lookups=0, seed=1, queries=28, pow_bits=16, ngroups=0, mode=0, ext=0, arities=()):
         """mode 0: degenerate circuit (every gate filter 0), `ngroups` selector groups (0: 3);
         mode 1: real circuit over the recursion gate set; mode 2: real circuit, small gate set
-        in one selector group."""
-        h = self.L.p2v_gen_circuit_new2(degree_bits, num_pis, lookups, seed, queries, pow_bits, ngroups, mode)
+        in one selector group.  ext / arities: the opt-in plonky2 conventions (P2V_EXT_*: 1 the
+        `arities` as fri_params.reduction_arity_bits under MinSize, 2 hiding salts, 4
+        hash_or_noop leaves; `arities` without 1: a Fixed strategy)."""
+        arr = (ctypes.c_int * max(1, len(arities)))(*arities)
+        h = self.L.p2v_gen_circuit_new3(degree_bits, num_pis, lookups, seed, queries, pow_bits, ngroups, mode, ext, arr, len(arities))
         if not h:
             raise RuntimeError(self.L.p2v_gen_last_error().decode())
         return GenCircuit(self, h)
@@ -187,8 +196,61 @@ def generator() -> Generator:
 
 
 @lru_cache(maxsize=16)
-def gen_circuit(degree_bits=6, num_pis=4, lookups=0, seed=1, queries=28, pow_bits=16, ngroups=0, mode=0) -> GenCircuit:
-    return generator().circuit(degree_bits, num_pis, lookups, seed, queries, pow_bits, ngroups, mode)
+def gen_circuit(degree_bits=6, num_pis=4, lookups=0, seed=1, queries=28, pow_bits=16, ngroups=0, mode=0, ext=0, arities=()) -> GenCircuit:
+    return generator().circuit(degree_bits, num_pis, lookups, seed, queries, pow_bits, ngroups, mode, ext, tuple(arities))
+
+
+# ----------------------------------------------------------------------------- plonky2 bytes
+def proof_bytes(proof_json: bytes, pi_prefix: bool = False) -> bytes:
+    """plonky2's binary serialization of a ProofWithPublicInputs (Write::
+    write_proof_with_public_inputs, restated here independently of the C++ reader in
+    csrc/circuit.cpp): u64 LE words, caps without length, Merkle proofs as a u8 count then the
+    hashes, circuit-sized vectors without length; public inputs raw, or after a u64 count."""
+    import struct
+    d = json.loads(proof_json)
+    pr, out = d["proof"], bytearray()
+
+    def f(x):
+        out.extend(struct.pack("<Q", int(x) % 0xFFFFFFFF00000001))
+
+    def cap(c):
+        for h in c:
+            for x in h["elements"]:
+                f(x)
+
+    def exts(v):
+        for a, b in v:
+            f(a)
+            f(b)
+
+    def mproof(sib):
+        out.append(len(sib["siblings"]))
+        cap(sib["siblings"])
+    cap(pr["wires_cap"])
+    cap(pr["plonk_zs_partial_products_cap"])
+    cap(pr["quotient_polys_cap"])
+    o = pr["openings"]
+    for k in ("constants", "plonk_sigmas", "wires", "plonk_zs", "plonk_zs_next", "lookup_zs", "lookup_zs_next",
+              "partial_products", "quotient_polys"):
+        exts(o[k])
+    fp = pr["opening_proof"]
+    for c in fp["commit_phase_merkle_caps"]:
+        cap(c)
+    for qr in fp["query_round_proofs"]:
+        for leaf, mp in qr["initial_trees_proof"]["evals_proofs"]:
+            for x in leaf:
+                f(x)
+            mproof(mp)
+        for st in qr["steps"]:
+            exts(st["evals"])
+            mproof(st["merkle_proof"])
+    exts(fp["final_poly"]["coeffs"])
+    f(fp["pow_witness"])
+    if pi_prefix:
+        out.extend(struct.pack("<Q", len(d["public_inputs"])))
+    for x in d["public_inputs"]:
+        f(x)
+    return bytes(out)
 
 
 # ----------------------------------------------------------------------------- mutations

@@ -1,0 +1,53 @@
+"""plonky2's binary proof serialization (p2v_pack_proof_bytes).  Parity
+unpinned: the reference has no binary reader (README.md:27) and no binary fixture exists
+offline.  The C++ reader (csrc/circuit.cpp) is checked against an independent Python writer
+(support.proof_bytes) through the JSON path: bytes -> packed words == JSON -> packed words, for
+std, lookup, real and P2V_EXT_* circuits, plus the truncation / shape error paths."""
+import numpy as np
+import pytest
+
+from support import gen_circuit, p2v_module, proof_bytes
+
+
+@pytest.mark.parametrize("args,ext", [((6, 4, 0, 1, 28, 8), 0), ((6, 0, 1, 2, 28, 8), 0), ((8, 4, 0, 1, 28, 8, 0, 1), 0),
+                                      ((6, 3, 0, 1, 28, 8, 0, 2, 6, (3, 1)), 6), ((6, 4, 0, 1, 28, 8, 0, 1, 7, (3, 2)), 7)])
+def test_bytes_pack_equals_json_pack(args, ext):
+    p2v = p2v_module()
+    gc = gen_circuit(*args)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey, ext)
+    for w, ps, fl in ((1, 1, 0), (2, 3, 0), (1, 5, 2)):
+        pr = gc.proof(w, ps, flags=fl)
+        ref = vk.pack(pr)
+        assert np.array_equal(vk.pack_bytes(proof_bytes(pr)), ref)
+        assert np.array_equal(vk.pack_bytes(proof_bytes(pr, pi_prefix=True)), ref)
+
+
+def test_bytes_error_paths():
+    p2v = p2v_module()
+    gc = gen_circuit(6, 4, 0, 1, 28, 8)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    b = proof_bytes(gc.proof(1, 1))
+    nbytes = 8 * (vk.info.proof_words) + vk.info.num_query_rounds * (4 + vk.info.num_fri_steps)
+    assert len(b) == nbytes   # every packed word once, plus one sibling-count byte per Merkle proof
+
+    def code(data):
+        with pytest.raises(p2v.P2VError) as e:
+            vk.pack_bytes(data)
+        return e.value.code
+    assert code(b[: len(b) // 2]) == p2v.E_PARSE                  # truncated inside the proof
+    assert code(b[:-8]) == p2v.E_SHAPE                            # one public input short
+    assert code(b + b"\0" * 8 * 3) == p2v.E_SHAPE                 # trailing words
+    i = 3 * 32 * 16 + 8 * 2 * (vk.info.num_openings_this + vk.info.num_openings_next) + 32 * 16 * vk.info.num_fri_steps
+    i += 8 * vk.info.oracle_widths[0]                             # first initial-tree sibling count
+    assert b[i] == vk.info.lde_bits - vk.info.cap_height
+    assert code(b[:i] + bytes([b[i] + 1]) + b[i + 1:]) == p2v.E_SHAPE
+    pre = proof_bytes(gc.proof(1, 1), pi_prefix=True)
+    bad = bytearray(pre)
+    bad[-8 * 5] ^= 1                                              # count 4 -> 5
+    assert code(bytes(bad)) == p2v.E_SHAPE
+    # values >= p are reduced like the JSON path reduces them
+    import struct
+    j = len(b) - 8
+    (x,) = struct.unpack("<Q", b[j:])
+    big = b[:j] + struct.pack("<Q", x + 0xFFFFFFFF00000001) if x < 0xFFFFFFFF else b
+    assert np.array_equal(vk.pack_bytes(big), vk.pack_bytes(b))

@@ -48,14 +48,14 @@ def test_gpu_matches_oracle_status_and_trace(p2v, nb, lk):
         assert np.array_equal(tr[i], otr), (i, np.nonzero(tr[i] != otr)[0][:10])
 
 
-def _gpu_vs_oracle(p2v, gc, cases, **kw):
+def _gpu_vs_oracle(p2v, gc, cases, ext=0, **kw):
     """Statuses and full traces of `cases` on the GPU equal the oracle's, word for word."""
     O = oracle()
-    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey, ext)
     res, tr = p2v.BatchVerifier(vk, 0, len(cases)).run(vk.pack_many(cases), trace=True, **kw)
     sts, otrs = [], []
     for i, proof in enumerate(cases):
-        st, otr = O.verify_json(gc.common, gc.vkey, proof, trace=True, **kw)
+        st, otr = O.verify_json(gc.common, gc.vkey, proof, trace=True, ext=ext, **kw)
         assert res[i] == st, (i, int(res[i]), st)
         assert np.array_equal(tr[i], otr), (i, np.nonzero(tr[i] != otr)[0][:10])
         sts.append(st)
@@ -78,6 +78,23 @@ def test_gpu_real_circuits_vs_oracle(p2v, mode, nb):
     off = trace_offsets(*circuit_shape(gc.common))
     r = circuit_shape(gc.common)[0]
     assert (otrs[:, off["combined"]: off["combined"] + 2 * r] != 0).all()
+
+
+@pytest.mark.parametrize("nb,mode,ext,arities", [(6, 1, 7, (3, 2)), (8, 1, 5, (1, 1, 1, 1)), (6, 2, 6, (3, 1)),
+                                                  (8, 1, 7, (3, 2, 1, 1)), (6, 0, 7, (2, 2, 1)), (6, 1, 4, (1, 1, 1)),
+                                                  (12, 1, 7, (4, 3, 2))])
+def test_gpu_ext_conventions_vs_oracle(p2v, nb, mode, ext, arities):
+    """Opt-in plonky2 conventions (include/p2v.h P2V_EXT_*; parity unpinned: the reference
+    implements none of them): MinSize / fri_params arities (incl. arity-2 and arity-8 steps),
+    salted leaves under hiding (hashed, then left out of combineInitial), hash_or_noop leaves
+    (arity-2 step leaves are 4 elements).  Valid proofs accept, the generator's malicious
+    modes reject, statuses and full traces equal the oracle's under the same flags."""
+    gc = gen_circuit(nb, 4, 0, 1, 28, 16, 0, mode, ext, arities)
+    cases = [gc.proof(1, 1), gc.proof(2, 2), gc.proof(1, 3, flags=1), gc.proof(1, 4, flags=2), gc.proof(2, 5, flags=4)]
+    if nb >= 12:
+        cases = cases[:3]
+    sts, _ = _gpu_vs_oracle(p2v, gc, cases, ext=ext)
+    assert sts == [1, 1, -3, 0, 0][:len(cases)]
 
 
 RANDOMIZED = {
