@@ -19,6 +19,7 @@ module Plonk.VerifierGPU
   , verifyProofBatchOn
   , GpuCircuit
   , loadGpuCircuit
+  , loadGpuCircuitExt
   , verifyWithCircuit
   , circuitWords
   , proofWords
@@ -28,7 +29,7 @@ import Control.Monad (when, forM_)
 import Data.Bits ((.&.))
 import Data.Char (ord)
 import Data.Int (Int8, Int32, Int64)
-import Data.Word (Word8, Word64)
+import Data.Word (Word8, Word32, Word64)
 import Foreign
 import Foreign.C.String (CString, peekCString)
 import Foreign.C.Types
@@ -48,6 +49,8 @@ data P2vCircuit
 
 foreign import ccall safe "p2v_circuit_from_words"
   c_circuit_from_words :: Ptr Word64 -> CSize -> Ptr (Ptr P2vCircuit) -> IO CInt
+foreign import ccall safe "p2v_circuit_from_words_ex"
+  c_circuit_from_words_ex :: Ptr Word64 -> CSize -> Word32 -> Ptr (Ptr P2vCircuit) -> IO CInt
 foreign import ccall safe "&p2v_circuit_free"
   c_circuit_free :: FunPtr (Ptr P2vCircuit -> IO ())
 foreign import ccall safe "p2v_circuit_get_info"
@@ -180,6 +183,15 @@ loadGpuCircuit vkey = withArrayLen (circuitWords vkey) $ \n ws ->
   alloca $ \out -> do
     rc <- c_circuit_from_words ws (fromIntegral n) out
     when (rc /= 0) $ throwLast "p2v_circuit_from_words"
+    GpuCircuit <$> (peek out >>= newForeignPtr c_circuit_free)
+
+-- | The same with opt-in plonky2 conventions the reference does not implement (P2V_EXT_* of
+-- include/p2v.h: 1 fri_params arities / MinSize, 2 hiding salts, 4 hash_or_noop leaves).
+loadGpuCircuitExt :: Word32 -> VerifierCircuitData -> IO GpuCircuit
+loadGpuCircuitExt ext vkey = withArrayLen (circuitWords vkey) $ \n ws ->
+  alloca $ \out -> do
+    rc <- c_circuit_from_words_ex ws (fromIntegral n) ext out
+    when (rc /= 0) $ throwLast "p2v_circuit_from_words_ex"
     GpuCircuit <$> (peek out >>= newForeignPtr c_circuit_free)
 
 -- | statuses: 1 True, 0 False, < 0 the reference's @error@ class (include/p2v.h)

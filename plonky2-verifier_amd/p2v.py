@@ -12,9 +12,13 @@ This module keeps that shape:
     ok    = verify_proof(vkey, proof)                                  # Plonk/Verifier.hs:56
 
 and adds the batch form the GPU is built for (verify_proof_batch / BatchVerifier).
-Where the reference raises `error` (failed Merkle proof, folding-step mismatch, shape
-mismatch, unsupported circuit) this module raises VerifierError with the same class;
-verify_proof returns False exactly where the reference returns False.
+Where the reference raises `error` (failed Merkle proof, folding-step mismatch, unsupported
+circuit) this module raises VerifierError with the same class, and verify_proof returns False
+where the reference returns False, for every proof whose list lengths are the ones the circuit
+implies.  Known divergence: a proof with another number of public inputs or
+final-polynomial coefficients raises P2VError(E_SHAPE) at pack time, where the reference hashes
+/ evaluates whatever it is given and returns False (with overwhelming probability: the
+transcript diverges); any other length mismatch is an `error` in the reference too.
 
 All verification runs in libp2v's HIP kernels on MI355X; there is no CPU fallback — on a
 machine without a GPU, verification raises P2VError(P2V_E_NODEVICE).
