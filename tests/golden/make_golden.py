@@ -33,6 +33,10 @@ CASES = [
     ("lookup_valid", 6, 1, 16, 1, 1, 0, None),
     ("lookup_wire", 6, 1, 16, 1, 2, 0, "wire"),
     ("n8_valid", 8, 0, 8, 3, 1, 0, None),
+    # the largest size the suite carries (LDE 2^19: initial paths of 15 siblings, 3 FRI steps);
+    # generating it takes ~80 s, so it is a fixture rather than generated in the GPU tests
+    ("n16_valid", 16, 0, 16, 1, 1, 0, None),
+    ("n16_step_sibling", 16, 0, 16, 1, 1, 0, "sib"),
 ]
 
 

@@ -241,3 +241,14 @@ def test_c_abi_host_example_packs_and_fails_loudly_without_gpu(tmp_path):
     if p2v.device_count() == 0:
         out = subprocess.run([exe] + args, capture_output=True, text=True)
         assert out.returncode == 5 and "no HIP device" in out.stderr
+
+
+def test_bench_refuses_mislabelled_gpu_count():
+    """bench.py --gpus N under a launcher whose WORLD_SIZE differs exits 2 before touching a GPU
+    (never print n_gpus for a run that did not use them)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--quick"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "refusing" in r.stderr
