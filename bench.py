@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """bench.py — Plonky2 proofs verified/sec on MI355X (BASELINE.json metric).
 
-One "step" = one pass of the verifier hot path (libp2v: transpose -> transcript + leaf
-hashing -> Merkle paths -> FRI queries -> vanishing/gates -> status) over one batch of
-4 096 standard-config proofs resident in HBM (BASELINE.json configs[1], "C2").  By
+One "step" = one pass of the verifier hot path (libp2v: transcript + leaf hashing ->
+Merkle paths -> FRI queries -> vanishing/gates -> status) over one batch of 4 096
+standard-config proofs resident in HBM (BASELINE.json configs[1], "C2"), in the 64-proof
+tiled layout (P2V_FLAG_INPUT_TILED; --layout proof-major for the row-per-proof form).  By
 default two batches are in flight per GPU (two verifier workspaces on two streams, the
 async NO_SYNC path of the C ABI), so one batch's latency-bound transcript overlaps the
 other's Merkle work; the one-at-a-time figure is reported alongside ("serial").  N GPUs =
@@ -15,7 +16,7 @@ config (degree_bits 12, rate_bits 3, cap_height 4, 28 queries, arity 16, PoW 16,
 80 routed, the 14-gate recursion gate set incl. Poseidon + CosetInterpolation).  By default a
 real circuit (gates on rows, selector polynomials, copy constraints, Z / partial products, a
 genuine quotient: every vanishing term non-zero at zeta; --circuit degenerate for the
-gate-filters-0 circuit, which --lookups uses).  D distinct proofs per rank tiled into distinct
+gate-filters-0 circuit, which --lookups uses).  D distinct proofs per rank repeated into distinct
 HBM memory, 1/16 of them corrupted (initial Merkle leaf -> -1, last step sibling -> -2).
 Every timed batch's statuses are checked against the expected vector.
 """
@@ -130,7 +131,7 @@ def kernel_bytes_model(info, trace_words):
     }
 
 
-def mutate_batch(tiled, info, every=16):
+def mutate_batch(rows, info, every=16):
     """Corrupt every `every`-th proof of the packed batch in place; returns the expected int8
     statuses.  Alternately (a) the first leaf word of query 0's constants/sigmas tree (initial
     Merkle check fails in round 0: status -1, Plonk/FRI.hs:108) and (b) the proof's last word,
@@ -146,10 +147,10 @@ def mutate_batch(tiled, info, every=16):
         logn -= a
         qstride += (2 << a) + 4 * max(0, logn - info.cap_height)
     q0 = W - Q * qstride   # query rounds are the layout's tail: [4 leaves | 4 paths | steps] each
-    expect = np.ones(tiled.shape[0], dtype=np.int8)
-    for k, i in enumerate(range(every // 2 - 1, tiled.shape[0], every)):
+    expect = np.ones(rows.shape[0], dtype=np.int8)
+    for k, i in enumerate(range(every // 2 - 1, rows.shape[0], every)):
         w = q0 if k % 2 == 0 else W - 1
-        tiled[i, w] = np.uint64((int(tiled[i, w]) + 1) % P)
+        rows[i, w] = np.uint64((int(rows[i, w]) + 1) % P)
         expect[i] = -1 if k % 2 == 0 else -2
     return expect
 
@@ -213,7 +214,7 @@ def ingest_rate(vk, proofs, threads):
 
 
 def json_rate(bvs, proofs, B, steps=3):
-    """End to end from JSON: B proof texts (the distinct ones tiled) in pinned host memory,
+    """End to end from JSON: B proof texts (the distinct ones repeated) in pinned host memory,
     copied to the device and packed there (p2v_verifier_run_json), then verified.  Serial:
     one batch at a time; pipelined: one host thread per verifier workspace, each on its own
     stream, so one batch's H2D copy overlaps another's packing and verification.  Reported
@@ -256,13 +257,13 @@ def json_rate(bvs, proofs, B, steps=3):
     return out
 
 
-def h2d_rate(bvs, tiled, B, expect, steps=3):
+def h2d_rate(bvs, rows, B, expect, steps=3):
     """PCIe-inclusive: packed proofs in pinned host memory, H2D copy inside the timed run.
     Serial: one batch at a time; pipelined (double-buffered): one host thread per verifier
     workspace, each on its own stream, so one batch's copy overlaps another's verification."""
     import threading
     import torch
-    host = torch.from_numpy(tiled.view(np.int64)).pin_memory()
+    host = torch.from_numpy(rows.view(np.int64)).pin_memory()
     arr = host.numpy().view(np.uint64)
     streams = [torch.cuda.Stream() for _ in bvs]
     for bv, st in zip(bvs, streams):
@@ -273,7 +274,7 @@ def h2d_rate(bvs, tiled, B, expect, steps=3):
     dt = (time.perf_counter() - t) / steps
     assert np.array_equal(res, expect)
     out = {"value": round(B / dt, 1), "unit": "proofs/s", "ms_per_step": round(dt * 1e3, 3),
-           "note": f"{B} proofs from pinned host memory per step, H2D {tiled.nbytes / 1e6:.0f} MB + verify + D2H, one batch at a time"}
+           "note": f"{B} proofs from pinned host memory per step, H2D {rows.nbytes / 1e6:.0f} MB + verify + D2H, one batch at a time"}
     if len(bvs) > 1:
         bad = []
 
@@ -290,7 +291,7 @@ def h2d_rate(bvs, tiled, B, expect, steps=3):
         dt = time.perf_counter() - t
         assert not bad
         out["pipelined"] = {"value": round(B * steps * len(bvs) / dt, 1), "inflight": len(bvs),
-                            "h2d_GBps_equiv": round(tiled.nbytes * steps * len(bvs) / dt / 1e9, 1)}
+                            "h2d_GBps_equiv": round(rows.nbytes * steps * len(bvs) / dt / 1e9, 1)}
     return out
 
 
@@ -298,18 +299,21 @@ C5_PROOFS = 1 << 20       # BASELINE.json configs[4]: 1M proofs over the node's 
 C5_CHUNK = 131072         # per launch: C5's per-GPU share on 8 GPUs
 
 
-def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, backend, dist, streams, steps=1):
+def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, backend, dist, streams, tiled, steps=1):
     """BASELINE.json configs[4] (C5): 1 048 576 std proofs sharded over the ranks (contiguous
     shards, p2v.shard_bounds), each rank verifying its shard in launches of up to 131 072 proofs
     (the per-GPU share at 8 GPUs) on two workspaces in flight.  The shard is device-resident:
-    the C2 batch tiled on the device to 131 072 distinct HBM rows, reused by every launch of
+    the C2 batch repeated on the device to 131 072 distinct HBM rows, reused by every launch of
     the shard.  Statuses of every launch are checked.  Time = max over ranks."""
     import torch
     s, e = p2v.shard_bounds(C5_PROOFS, world, int(os.environ.get("RANK", "0")))
     n = e - s
     rows = min(C5_CHUNK, n)
     reps = (rows + B - 1) // B
-    big = d_proofs.repeat(reps, 1)[:rows].contiguous()
+    if tiled:   # whole 64-proof tiles of the tiled batch, repeated (proof order is preserved)
+        big = d_proofs.repeat(reps)[: (rows + 63) // 64 * 64 * info.proof_words].contiguous()
+    else:
+        big = d_proofs.repeat(reps, 1)[:rows].contiguous()
     exp = d_expect.repeat(reps)[:rows]
     bvs = [p2v.BatchVerifier(vk, local, rows) for _ in range(2)]
     res = [torch.empty(rows, dtype=torch.int8, device=dev) for _ in range(2)]
@@ -317,7 +321,8 @@ def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, backend, dis
 
     def one_pass():
         for i, c in enumerate(chunks):
-            bvs[i % 2].run_device(big.data_ptr(), c, res[i % 2].data_ptr(), stream=streams[i % 2 % len(streams)].cuda_stream, sync=False)
+            bvs[i % 2].run_device(big.data_ptr(), c, res[i % 2].data_ptr(), stream=streams[i % 2 % len(streams)].cuda_stream, sync=False,
+                                  tiled=tiled)
     one_pass()   # warm-up
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -348,16 +353,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=None,
                     help="GPUs (= ranks). Under torchrun it must equal WORLD_SIZE; without torchrun and N > 1 "
                          "bench.py starts the N ranks itself (torch.distributed.run child process)")
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)   # ~0.5 s timed: long enough for an external utilisation sampler
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096, help="proofs per GPU per step")
-    ap.add_argument("--distinct", type=int, default=64, help="distinct generated proofs per rank (tiled)")
+    ap.add_argument("--distinct", type=int, default=64, help="distinct generated proofs per rank (repeated to the batch)")
     ap.add_argument("--witnesses", type=int, default=8)
     ap.add_argument("--circuit", choices=("real", "degenerate"), default="real",
                     help="real: gates on rows, copy constraints, genuine quotient (C4's recursion gate set); "
                          "degenerate: gate filters 0 (required with --lookups: the real prover has no lookup argument)")
     ap.add_argument("--degree-bits", type=int, default=12)
     ap.add_argument("--inflight", type=int, default=2, help="batches in flight per GPU (workspaces/streams)")
+    ap.add_argument("--layout", choices=("tiled", "proof-major"), default="tiled",
+                    help="device-resident batch layout: 64-proof tiles (P2V_FLAG_INPUT_TILED, coalesced loads) or proof-major rows")
     ap.add_argument("--lookups", type=int, default=0,
                     help="0: standard recursion circuit (C2); 2: + LookupGate/LookupTableGate with a 256-entry and a 2^16-entry table (C3 circuit)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -405,12 +412,13 @@ def main():
     info = vk.info
     packed = vk.pack_many(proofs)
     B = args.batch
-    tiled = np.ascontiguousarray(packed[np.arange(B) % len(proofs)])
+    rows = np.ascontiguousarray(packed[np.arange(B) % len(proofs)])
     # 1/16 of the batch is corrupted: the GPU does the same work for them, and
     # the statuses of every timed batch are checked against the expected vector
-    expect = mutate_batch(tiled, info)
+    expect = mutate_batch(rows, info)
     dev = torch.device("cuda", local)
-    d_proofs = torch.from_numpy(tiled.view(np.int64)).to(dev)
+    lay_tiled = args.layout == "tiled"
+    d_proofs = torch.from_numpy((p2v.tile_proofs(rows) if lay_tiled else rows).view(np.int64)).to(dev)
     d_expect = torch.from_numpy(expect).to(dev)
     nv = max(1, args.inflight)
     d_res = [torch.empty(B, dtype=torch.int8, device=dev) for _ in range(nv)]
@@ -428,7 +436,8 @@ def main():
         t = time.perf_counter()
         for i in range(k):
             j = i % nv if pipelined else 0
-            bvs[j].run_device(d_proofs.data_ptr(), B, d_res[j].data_ptr(), stream=streams[j].cuda_stream, sync=not pipelined)
+            bvs[j].run_device(d_proofs.data_ptr(), B, d_res[j].data_ptr(), stream=streams[j].cuda_stream, sync=not pipelined,
+                              tiled=lay_tiled)
             if not pipelined:
                 for name, v in bvs[0].last_timings().items():
                     ktimes.setdefault(name, []).append(v)
@@ -442,7 +451,8 @@ def main():
         return float(tmax.item()), ktimes
 
     for i in range(args.warmup):
-        bvs[i % nv].run_device(d_proofs.data_ptr(), B, d_res[i % nv].data_ptr(), stream=streams[i % nv].cuda_stream, sync=False)
+        bvs[i % nv].run_device(d_proofs.data_ptr(), B, d_res[i % nv].data_ptr(), stream=streams[i % nv].cuda_stream, sync=False,
+                               tiled=lay_tiled)
     torch.cuda.synchronize(dev)
     assert all(bool((r == d_expect).all()) for r in d_res[:max(1, min(nv, args.warmup))]), "batch statuses differ from the expected ones"
     # serial pass: per-kernel durations (HIP events recorded on the run's streams inside libp2v)
@@ -460,7 +470,7 @@ def main():
     kavg = {k: float(np.mean(v)) for k, v in ktimes.items()}
     c5 = None
     if not args.quick and not args.no_c5:
-        c5 = c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, args.dist_backend, dist, streams)
+        c5 = c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, args.dist_backend, dist, streams, lay_tiled)
     if rank == 0:
         kb = kernel_bytes_model(info, info.trace_words)
         # dominant kernel: the longest launch on the main stream (k_transcript / k_vanish / k_fri /
@@ -489,7 +499,8 @@ def main():
             "config": {"workload": f"{'C3' if args.lookups else 'C2'}: {B} std-config Plonky2 proofs per GPU per step (degree_bits {info.degree_bits}, "
                                    f"{'real circuit of the recursion gate set, ' if real else 'degenerate circuit, '}"
                                    f"28 FRI queries, arity 16, deg-2 ext{', lookups: 256 + 65536-entry tables' if args.lookups > 1 else (', lookups' if args.lookups else '')}), "
-                                   f"{len(proofs)} distinct tiled, 1/16 corrupted, device-resident",
+                                   f"{len(proofs)} distinct repeated, 1/16 corrupted, device-resident"
+                                   f"{' in 64-proof tiles' if lay_tiled else ' proof-major'}",
                        "global_batch": B * world, "degree_bits": info.degree_bits, "parallelism": f"proof-sharded x{world}",
                        "inflight": nv},
             "serial": {"value": round(total / dt_serial, 1), "ms_per_step": round(dt_serial / args.steps * 1e3, 4),
@@ -507,7 +518,7 @@ def main():
             out["c5"] = c5
         if world == 1 and not args.quick:
             out["ingest"] = ingest_rate(vk, proofs, threads)
-            out["h2d_end_to_end"] = h2d_rate(bvs, tiled, B, expect)
+            out["h2d_end_to_end"] = h2d_rate(bvs, rows, B, expect)
             out["json_end_to_end"] = json_rate(bvs, proofs, B)
         if world == 1 and not args.no_cpu_baseline and not args.quick:
             out["cpu_baseline"] = cpu_baseline(gc, proofs, threads)

@@ -187,10 +187,20 @@ int  p2v_pack_proof_bytes(const p2v_circuit* c, const uint8_t* bytes, size_t n, 
 #define P2V_FLAG_INPUT_DEVICE  1u  /* `proofs` is a device pointer on the verifier's device  */
 #define P2V_FLAG_RESULT_DEVICE 2u  /* `results` (and trace) are device pointers              */
 #define P2V_FLAG_NO_SYNC       4u  /* do not synchronise the stream before returning          */
+#define P2V_FLAG_INPUT_TILED  16u  /* `proofs` is in the 64-proof tiled layout below (p2v_tile_proofs) instead of
+                                      proof-major: every wave's loads are then whole 512-B rows          */
 #define P2V_FLAG_UNIT_FILTERS  8u  /* parity mode: every gate filter and lookup selector := 1, so the
                                       trace's combined values C_i expose every constraint program
                                       (the oracle's or_verify full_trace bit 1); statuses are then
                                       meaningless.  Tests only. */
+
+/* Tiled batch layout (P2V_FLAG_INPUT_TILED): word w of proof i at
+ *   tiled[((i / 64) * proof_words + w) * 64 + i % 64],
+ * i.e. ceil(n / 64) tiles of [proof_words][64]; a tile's rows past n are never read (lanes past n
+ * re-read proof n - 1, as in the proof-major form).  The packed values are the same; only their
+ * order differs, so a packer can write either.  p2v_tiled_words gives the buffer size in u64. */
+size_t p2v_tiled_words(size_t n, size_t proof_words);
+void   p2v_tile_proofs(const uint64_t* proof_major, size_t n, size_t proof_words, uint64_t* tiled);   /* host; pads with 0 */
 
 int  p2v_device_count(void);
 

@@ -403,7 +403,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
 #undef UP
   const size_t B = v->Bmax;
   const size_t chw = (size_t)(4 + 7 * d.r + 4 + 2 * d.S + 1 + d.Q + 4);
-  if (e == hipSuccess) e = v->in.alloc((size_t)L.words * max_batch * 8);
+  if (e == hipSuccess) e = v->in.alloc((size_t)L.words * v->Bmax * 8);   // whole 64-proof tiles (P2V_FLAG_INPUT_TILED)
   if (e == hipSuccess && !P2V_PROOF_MAJOR) e = v->soa.alloc((size_t)L.words * B * 8);   // the transposed batch
   if (e == hipSuccess) e = v->chal.alloc(chw * B * 8);
   if (e == hipSuccess) e = v->leafdig.alloc((size_t)d.Q * d.T * 4 * B * 8);
@@ -443,6 +443,21 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   return P2V_OK;
 }
 
+size_t p2v_tiled_words(size_t n, size_t proof_words) { return (n + 63) / 64 * 64 * proof_words; }
+
+void p2v_tile_proofs(const uint64_t* pm, size_t n, size_t W, uint64_t* tiled) {
+  if (!pm || !tiled) return;
+  const size_t tiles = (n + 63) / 64;
+  for (size_t t = 0; t < tiles; t++) {
+    uint64_t* dst = tiled + t * W * 64;
+    for (size_t w = 0; w < W; w++)
+      for (size_t l = 0; l < 64; l++) {
+        const size_t i = t * 64 + l;
+        dst[w * 64 + l] = i < n ? pm[i * W + w] : 0;
+      }
+  }
+}
+
 int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* results, uint64_t* trace, void* stream_, uint32_t flags) {
   if (!v || (!proofs && n) || !results) return fail(P2V_E_ARG, "null argument");
   if (n > v->max_batch) return fail(P2V_E_ARG, "batch larger than max_batch");
@@ -453,11 +468,15 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   DevCircuit d = v->dc;
   d.n = (int)n;
   d.unit_filters = (flags & P2V_FLAG_UNIT_FILTERS) ? 1 : 0;
+  d.tiled = (flags & P2V_FLAG_INPUT_TILED) ? 1 : 0;
+  d.wstride = d.tiled ? 64 : 1;
+  if (d.tiled && !P2V_PROOF_MAJOR) return fail(P2V_E_ARG, "P2V_FLAG_INPUT_TILED needs the in-place build (P2V_PROOF_MAJOR=1)");
   d.B = (int)((n + 63) / 64 * 64);
   const int64_t words = C.L.words;
   const uint64_t* src = proofs;
   if (!(flags & P2V_FLAG_INPUT_DEVICE)) {
-    HCK(hipMemcpyAsync(v->in.p, proofs, (size_t)words * n * 8, hipMemcpyHostToDevice, st));
+    const size_t in_words = d.tiled ? p2v_tiled_words(n, (size_t)words) : (size_t)words * n;
+    HCK(hipMemcpyAsync(v->in.p, proofs, in_words * 8, hipMemcpyHostToDevice, st));
     src = (const uint64_t*)v->in.p;
   }
   int8_t* dres = (flags & P2V_FLAG_RESULT_DEVICE) ? results : (int8_t*)v->res.p;

@@ -237,7 +237,15 @@ static void finalize_circuit(Circuit& C) {
   const int ngroups = (int)C.grp_start.size();
   const int nluts = (int)C.lut_in.size();
   if (C.r <= 0 || C.r > 4) throw CircuitError("num_challenges must be in 1..4 (this build)");
-  if (C.cap_height < 0 || C.cap_height > 20 || C.degree_bits <= 0 || C.lde_bits > 30) throw CircuitError("unsupported FRI sizes");
+  if (C.cap_height < 0 || C.cap_height > 20 || C.degree_bits <= 0 || C.rate_bits < 0 || C.lde_bits > 30) throw CircuitError("unsupported FRI sizes");
+  // this build's size limits (far above any Plonky2 config; they keep every derived size in range)
+  constexpr int kMaxCount = 1 << 20;
+  auto in_range = [](int64_t v, int64_t lo, int64_t hi) { return v >= lo && v <= hi; };
+  if (!in_range(C.num_wires, 1, kMaxCount) || !in_range(C.num_routed, 0, C.num_wires) || !in_range(C.num_gate_consts, 0, kMaxCount) ||
+      !in_range(C.num_constants, 0, kMaxCount) || !in_range(C.num_pis, 0, kMaxCount) || !in_range(C.npp, 0, kMaxCount) ||
+      !in_range(C.nlp, 0, kMaxCount) || !in_range(C.nls, 0, kMaxCount) || !in_range(C.qdf, 0, 1 << 10) ||
+      !in_range(C.num_queries, 0, 1 << 10) || !in_range(C.pow_bits, 0, 64) || (int64_t)C.lut_in.size() > kMaxCount)
+    throw CircuitError("circuit sizes beyond this build's limits (DESIGN.md §8)");
   if (C.nls != (nluts == 0 ? 0 : 4 + nluts)) throw CircuitError("getSelectorConfig: fatal: num_lookup_selectors /= (4 + #nluts)");
   if (C.num_constants != ngroups + C.nls + C.num_gate_consts) throw CircuitError("getSelectorConfig: fatal: constant columns tally does not add up!");
   C.n_gate_eval = (int)std::min(C.sel_idx.size(), C.gates.size());

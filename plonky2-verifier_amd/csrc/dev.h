@@ -20,6 +20,8 @@ struct DevCircuit {
   int32_t width[4];                // data columns per initial oracle (combineInitial)
   int32_t lwidth[4];               // packed leaf words (width + salts under P2V_EXT_HIDING): the sponged row
   int32_t noop_leaves;             // P2V_EXT_HASH_OR_NOOP: a leaf of <= 4 words is its own digest
+  int32_t tiled;                   // P2V_FLAG_INPUT_TILED: the batch is [n/64][words][64] (devcommon.h ld())
+  int64_t wstride;                 // distance between a proof's consecutive words: 64 tiled, else 1
   // tree t of each unit position, most expensive first, so long waves dispatch first and short
   // ones fill the tail: leaf hashing by sponge length, Merkle paths by depth
   int8_t leaf_order[4 + P2V_MAX_STEPS], merkle_order[4 + P2V_MAX_STEPS];

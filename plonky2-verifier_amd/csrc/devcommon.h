@@ -16,9 +16,17 @@ using gl::E;
 #ifndef P2V_PROOF_MAJOR
 #define P2V_PROOF_MAJOR 1
 #endif
+//
+// c.tiled (P2V_FLAG_INPUT_TILED, wave-uniform): the caller's batch in 64-proof tiles
+// [n/64][words][64], so the 64 lanes of a wave read one 512-B row per word: the same kernels with
+// coalesced loads and no transpose pass, and HBM traffic at the algorithmic bytes.
+// Both forms are affine in w, addr = base(p) + w * c.wstride (wstride 1 or 64, wave-uniform), so
+// a kernel keeps one per-lane base and a scalar step, as the proof-major form alone did.
 __device__ __forceinline__ uint64_t ld(const DevCircuit& c, int64_t w, int p) {
 #if P2V_PROOF_MAJOR
-  return c.soa[(int64_t)min(p, c.n - 1) * c.words + w];
+  const int64_t q = min(p, c.n - 1);
+  const int64_t base = c.tiled ? (((q >> 6) * c.words) << 6) + (q & 63) : q * c.words;
+  return c.soa[base + w * c.wstride];
 #else
   return c.soa[w * c.B + p];
 #endif

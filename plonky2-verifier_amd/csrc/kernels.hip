@@ -338,10 +338,10 @@ extern "C" __global__ void __launch_bounds__(256) k_merkle(DevCircuit c) {
   uint64_t cur[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) cur[i] = src[(int64_t)i * c.B];
-  // one level's 32 B of siblings per load: loading two levels at once (82 VGPRs) would cost a
-  // wave per SIMD (6 -> 5); the line re-fetches this leaves are served by the Infinity Cache
   for (int l = 0; l < depth; l++) {   // even index: compress(cur, sib), odd: compress(sib, cur)
     uint64_t sib[4];
+    // one level's 32 B of siblings per load (proof-major: the line re-fetches this leaves hit
+    // the Infinity Cache; tiled: whole 512-B rows per wave)
 #pragma unroll
     for (int i = 0; i < 4; i++) sib[i] = ld(c, poff + 4 * l + i, p);
     const bool odd = idx & 1u;

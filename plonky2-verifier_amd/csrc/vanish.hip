@@ -565,7 +565,11 @@ __device__ __forceinline__ void vanish_body(const DevCircuit& c) {
   __builtin_amdgcn_s_setprio(2);
   vanish_item<CLS>(c, it, p);
 }
-extern "C" __global__ void __launch_bounds__(256) k_vanish_poseidon(DevCircuit c) { vanish_body<VK_POSEIDON>(c); }
+// waves_per_eu(2, 2): left alone, the compiler spills 36-68 B/lane to reach 3 waves/SIMD at the same
+// 164 VGPRs; a batch has fewer Poseidon-part waves (8 per 64 proofs) than SIMDs, so 2 costs nothing
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_vanish_poseidon(DevCircuit c) {
+  vanish_body<VK_POSEIDON>(c);
+}
 extern "C" __global__ void __launch_bounds__(256) k_vanish_coset(DevCircuit c) { vanish_body<VK_COSET>(c); }
 extern "C" __global__ void __launch_bounds__(256) k_vanish(DevCircuit c) { vanish_body<VK_MISC>(c); }
 

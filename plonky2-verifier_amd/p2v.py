@@ -65,6 +65,7 @@ FLAG_INPUT_DEVICE = 1
 FLAG_RESULT_DEVICE = 2
 FLAG_NO_SYNC = 4
 FLAG_UNIT_FILTERS = 8   # parity mode (tests only): every gate filter / lookup selector := 1
+FLAG_INPUT_TILED = 16   # the batch in 64-proof tiles [n/64][words][64] (tile_proofs)
 
 
 class P2VError(RuntimeError):
@@ -118,6 +119,10 @@ def lib() -> ctypes.CDLL:
     L.p2v_circuit_from_words_ex.argtypes = [u64p, sz, ctypes.c_uint32, ctypes.POINTER(vp)]
     L.p2v_pack_proof_words.argtypes = [vp, u64p, sz, u64p]
     L.p2v_pack_proof_bytes.argtypes = [vp, ctypes.c_char_p, sz, u64p]
+    L.p2v_tiled_words.argtypes = [sz, sz]
+    L.p2v_tiled_words.restype = sz
+    L.p2v_tile_proofs.argtypes = [u64p, sz, sz, u64p]
+    L.p2v_tile_proofs.restype = None
     L.p2v_device_count.argtypes = []
     L.p2v_verifier_create.argtypes = [vp, ctypes.c_int, sz, ctypes.POINTER(vp)]
     L.p2v_verifier_free.argtypes = [vp]
@@ -287,17 +292,20 @@ class BatchVerifier:
         _check(lib().p2v_verifier_create(circuit.handle, device, max_batch, ctypes.byref(h)))
         self._h = h
 
-    def run(self, proofs: np.ndarray, trace: bool = False, unit_filters: bool = False, stream: int = 0):
+    def run(self, proofs: np.ndarray, trace: bool = False, unit_filters: bool = False, stream: int = 0,
+            tiled: bool = False):
         """proofs: uint64 [n, proof_words] host array.  Returns int8 statuses (and trace).
         unit_filters: parity mode (P2V_FLAG_UNIT_FILTERS), statuses meaningless.  stream: a
-        hipStream_t handle (0: the default stream)."""
+        hipStream_t handle (0: the default stream).  tiled: the batch goes to the device in the
+        64-proof tiled layout (P2V_FLAG_INPUT_TILED; tiled here with tile_proofs)."""
         proofs = np.ascontiguousarray(proofs, dtype=np.uint64)
         n = proofs.shape[0]
+        src = tile_proofs(proofs) if tiled else proofs
         res = np.empty(n, dtype=np.int8)
         tr = np.empty((n, self.circuit.info.trace_words), dtype=np.uint64) if trace else None
-        _check(lib().p2v_verifier_run(self._h, proofs.ctypes.data, n, res.ctypes.data,
-                                      tr.ctypes.data if trace else None, ctypes.c_void_p(stream) if stream else None,
-                                      FLAG_UNIT_FILTERS if unit_filters else 0))
+        flags = (FLAG_UNIT_FILTERS if unit_filters else 0) | (FLAG_INPUT_TILED if tiled else 0)
+        _check(lib().p2v_verifier_run(self._h, src.ctypes.data, n, res.ctypes.data,
+                                      tr.ctypes.data if trace else None, ctypes.c_void_p(stream) if stream else None, flags))
         return (res, tr) if trace else res
 
     @staticmethod
@@ -341,10 +349,11 @@ class BatchVerifier:
         return words, codes
 
     def run_device(self, proofs_ptr: int, n: int, results_ptr: int, stream: int = 0, trace_ptr: int = 0,
-                   sync: bool = True) -> None:
+                   sync: bool = True, tiled: bool = False) -> None:
         """Device-resident batch: raw device pointers (e.g. torch tensor .data_ptr()) and a
-        hipStream_t handle (torch.cuda.current_stream().cuda_stream)."""
-        flags = FLAG_INPUT_DEVICE | FLAG_RESULT_DEVICE | (0 if sync else FLAG_NO_SYNC)
+        hipStream_t handle (torch.cuda.current_stream().cuda_stream).  tiled: the batch is in the
+        64-proof tiled layout (P2V_FLAG_INPUT_TILED, tile_proofs)."""
+        flags = FLAG_INPUT_DEVICE | FLAG_RESULT_DEVICE | (0 if sync else FLAG_NO_SYNC) | (FLAG_INPUT_TILED if tiled else 0)
         _check(lib().p2v_verifier_run(self._h, ctypes.c_void_p(proofs_ptr), n, ctypes.c_void_p(results_ptr),
                                       ctypes.c_void_p(trace_ptr) if trace_ptr else None, ctypes.c_void_p(stream), flags))
 
@@ -361,6 +370,18 @@ class BatchVerifier:
                 self._h = ctypes.c_void_p()
         except Exception:
             pass
+
+
+def tile_proofs(packed: np.ndarray) -> np.ndarray:
+    """Proof-major packed rows [n, proof_words] -> the 64-proof tiled layout of
+    P2V_FLAG_INPUT_TILED (include/p2v.h): ceil(n/64) tiles of [proof_words][64], padded with 0.
+    Flat uint64 array of p2v_tiled_words(n, proof_words) words."""
+    packed = np.ascontiguousarray(packed, dtype=np.uint64)
+    n, W = packed.shape
+    t = (n + 63) // 64
+    pad = np.zeros((t * 64, W), dtype=np.uint64)
+    pad[:n] = packed
+    return np.ascontiguousarray(pad.reshape(t, 64, W).transpose(0, 2, 1)).reshape(-1)
 
 
 def _status_to_bool(st: int) -> bool:

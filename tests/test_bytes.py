@@ -51,3 +51,33 @@ def test_bytes_error_paths():
     (x,) = struct.unpack("<Q", b[j:])
     big = b[:j] + struct.pack("<Q", x + 0xFFFFFFFF00000001) if x < 0xFFFFFFFF else b
     assert np.array_equal(vk.pack_bytes(big), vk.pack_bytes(b))
+
+
+def test_bytes_fuzz_never_crashes():
+    """Seeded truncations and byte flips of a binary proof: the reader returns OK, E_PARSE or
+    E_SHAPE, never reads past the buffer (ASan-free host build, so a crash would show here)."""
+    import random
+    p2v = p2v_module()
+    gc = gen_circuit(6, 4, 1, 1, 28, 8)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    b = proof_bytes(gc.proof(1, 1))
+    rnd = random.Random(7)
+    seen = set()
+    for _ in range(300):
+        d = bytearray(b)
+        op = rnd.randrange(3)
+        if op == 0:
+            d = d[: rnd.randrange(len(d))]
+        elif op == 1:
+            for _ in range(rnd.randrange(1, 6)):
+                d[rnd.randrange(len(d))] = rnd.randrange(256)
+        else:
+            i = rnd.randrange(len(d))
+            d = d[:i] + bytes(rnd.randrange(1, 40)) + d[i:]
+        try:
+            vk.pack_bytes(bytes(d))
+            seen.add(0)
+        except p2v.P2VError as e:
+            assert e.code in (p2v.E_PARSE, p2v.E_SHAPE), e
+            seen.add(e.code)
+    assert {p2v.E_PARSE, p2v.E_SHAPE} <= seen

@@ -12,7 +12,7 @@ import os
 import numpy as np
 import pytest
 
-from support import GOLDEN, gen_circuit, mutate, oracle, p2v_module
+from support import GOLDEN, P, gen_circuit, mutate, oracle, p2v_module
 
 pytestmark = pytest.mark.gpu
 
@@ -175,6 +175,30 @@ def test_gpu_n12_standard_batch_vs_oracle(p2v):
             st, otr = O.verify_json(gc.common, gc.vkey, pool[k], trace=True)
             assert np.array_equal(tr[lanes[0]], otr)
             assert (tr[lanes] == tr[lanes[0]]).all()
+
+
+@pytest.mark.parametrize("nb,mode,lk", [(6, 1, 0), (6, 0, 2), (8, 1, 0)])
+def test_gpu_tiled_input_matches_proof_major(p2v, nb, mode, lk):
+    """P2V_FLAG_INPUT_TILED (the bench's layout): the same proofs in 64-proof tiles give the
+    same statuses and full traces as the proof-major rows, host and device entry points, on a
+    ragged batch (100 proofs: a partial last tile) with corrupted proofs in it."""
+    import torch
+    gc = gen_circuit(nb, 4, lk, 1, 28, 16, 0, mode)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    pool = [gc.proof(1, 1), gc.proof(2, 2), gc.proof(1, 3, flags=1), gc.proof(1, 4, flags=2)]
+    packed = vk.pack_many(pool)
+    rows = np.ascontiguousarray(packed[np.arange(100) % len(pool)])
+    rows[37, vk.info.proof_words - 1] = (int(rows[37, vk.info.proof_words - 1]) + 1) % P   # last step sibling: -2
+    bv = p2v.BatchVerifier(vk, 0, 100)
+    r0, t0 = bv.run(rows, trace=True)
+    r1, t1 = bv.run(rows, trace=True, tiled=True)
+    assert np.array_equal(r0, r1) and np.array_equal(t0, t1)
+    assert r0[37] == -2 and set(r0[:4].tolist()) == {1, -3, 0}
+    d = torch.from_numpy(p2v.tile_proofs(rows).view(np.int64)).cuda()
+    dres = torch.empty(100, dtype=torch.int8, device="cuda")
+    bv.run_device(d.data_ptr(), 100, dres.data_ptr(), stream=torch.cuda.current_stream().cuda_stream, tiled=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(dres.cpu().numpy(), r0)
 
 
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 257])

@@ -252,3 +252,36 @@ def test_bench_refuses_mislabelled_gpu_count():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--quick"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "refusing" in r.stderr
+
+
+def test_host_readers_under_asan_and_ubsan(tmp_path):
+    """tools/asan/run.sh: every host reader (JSON circuit / proof, template packer, words, bytes)
+    built with -fsanitize=address,undefined and fed seeded mutations of real inputs; any memory
+    error, leak or UB aborts the run (host code only: no GPU sanitizers on this pool)."""
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    env = dict(os.environ, ITERS="300", OUT=str(tmp_path))
+    r = subprocess.run(["bash", os.path.join(ROOT, "tools", "asan", "run.sh")], env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["other"] == 0 and res["ok"] > 0 and res["parse"] > 0 and res["shape"] > 0
+
+
+def test_tiled_layout_host_helpers():
+    """P2V_FLAG_INPUT_TILED layout (include/p2v.h): the C helper and p2v.tile_proofs agree, and
+    word w of proof i sits at ((i // 64) * W + w) * 64 + i % 64."""
+    p2v = p2v_module()
+    rng = np.random.default_rng(3)
+    for n, W in ((1, 7), (64, 5), (100, 13), (130, 3)):
+        pm = rng.integers(0, 2**63, size=(n, W), dtype=np.uint64)
+        t = p2v.tile_proofs(pm)
+        assert t.size == p2v.lib().p2v_tiled_words(n, W)
+        c = np.zeros(t.size, dtype=np.uint64)
+        p2v.lib().p2v_tile_proofs(pm.ctypes.data, n, W, c.ctypes.data)
+        assert np.array_equal(t, c)
+        for i in (0, n // 2, n - 1):
+            for w in (0, W - 1):
+                assert t[((i // 64) * W + w) * 64 + i % 64] == pm[i, w]
