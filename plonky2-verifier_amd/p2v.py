@@ -384,6 +384,96 @@ def tile_proofs(packed: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(pad.reshape(t, 64, W).transpose(0, 2, 1)).reshape(-1)
 
 
+# ----------------------------------------------------------------------------- intermediates
+# The reference's driver (src/testmain.hs:54-63) prints the sub-results of verifyProof:
+# proofChallenges, evalCombinedPlonkConstraints and checkCombinedPlonkEquations'.  The same values,
+# computed by the GPU kernels of the batch path, come out of libp2v's per-proof trace
+# (include/p2v.h "debug trace layout"); these mirror those functions.
+FExt = tuple   # (re, im), GoldilocksExt.hs:24-32
+
+
+def trace_offsets(r: int, S: int, Q: int) -> dict:
+    """Word offsets of the per-proof trace (include/p2v.h)."""
+    o = {"pi_hash": 0, "betas": 4}
+    o["gammas"] = o["betas"] + r
+    o["alphas"] = o["gammas"] + r
+    o["deltas"] = o["alphas"] + r
+    o["zeta"] = o["deltas"] + 4 * r
+    o["fri_alpha"] = o["zeta"] + 2
+    o["fri_betas"] = o["fri_alpha"] + 2
+    o["pow"] = o["fri_betas"] + 2 * S
+    o["query_idx"] = o["pow"] + 1
+    o["combined"] = o["query_idx"] + Q
+    o["quotient"] = o["combined"] + 2 * r
+    o["q_initial"] = o["quotient"] + 2 * r
+    o["q_folded"] = o["q_initial"] + 2 * Q
+    o["q_final"] = o["q_folded"] + 2 * Q
+    o["flags"] = o["q_final"] + 2 * Q
+    o["lut_re"] = o["flags"] + 1
+    return o
+
+
+@dataclass(frozen=True)
+class FriChallenges:   # Challenge/FRI.hs:24-30
+    fri_alpha: FExt
+    fri_betas: tuple
+    fri_pow_response: int
+    fri_query_indices: tuple
+
+
+@dataclass(frozen=True)
+class ProofChallenges:   # Challenge/Verifier.hs:45-53
+    plonk_betas: tuple
+    plonk_gammas: tuple
+    plonk_alphas: tuple
+    plonk_deltas: tuple      # per round (A, B, alpha, delta) = chunksOf 4 (betas ++ gammas ++ new), :36-40; () without lookups
+    plonk_zeta: FExt
+    fri_challenges: FriChallenges
+    public_inputs_hash: tuple
+
+
+def _trace_one(vkey: VerifierCircuitData, proof, device: int) -> np.ndarray:
+    text = proof.json if isinstance(proof, ProofWithPublicInputs) else _bytes(proof)
+    bv = BatchVerifier(vkey, device, 1)
+    _res, tr = bv.run(vkey.pack(text)[None, :], trace=True)
+    return tr[0]
+
+
+def _ext(tr, o) -> FExt:
+    return (int(tr[o]), int(tr[o + 1]))
+
+
+def proof_challenges(vkey: VerifierCircuitData, proof, device: int = 0) -> ProofChallenges:
+    """proofChallenges (Challenge/Verifier.hs:58-103): the Fiat-Shamir challenges of one proof,
+    as the GPU transcript derives them."""
+    inf = vkey.info
+    r, S, Q = inf.num_challenges, inf.num_fri_steps, inf.num_query_rounds
+    tr, o = _trace_one(vkey, proof, device), trace_offsets(r, S, Q)
+    rng = lambda k, n: tuple(int(x) for x in tr[o[k]: o[k] + n])   # noqa: E731
+    deltas = tuple(rng("deltas", 4 * r)[4 * i: 4 * i + 4] for i in range(r)) if inf.has_lookups else ()
+    fri = FriChallenges(_ext(tr, o["fri_alpha"]), tuple(_ext(tr, o["fri_betas"] + 2 * i) for i in range(S)),
+                        int(tr[o["pow"]]), rng("query_idx", Q))
+    return ProofChallenges(rng("betas", r), rng("gammas", r), rng("alphas", r), deltas, _ext(tr, o["zeta"]), fri,
+                           rng("pi_hash", 4))
+
+
+def eval_combined_plonk_constraints(vkey: VerifierCircuitData, proof, device: int = 0) -> List[FExt]:
+    """evalCombinedPlonkConstraints (Plonk/Vanishing.hs:48-51): the vanishing terms at zeta
+    combined with powers of each round's alpha, one F^2 value per challenge round."""
+    inf = vkey.info
+    r = inf.num_challenges
+    tr, o = _trace_one(vkey, proof, device), trace_offsets(r, inf.num_fri_steps, inf.num_query_rounds)
+    return [_ext(tr, o["combined"] + 2 * i) for i in range(r)]
+
+
+def check_combined_plonk_equations(vkey: VerifierCircuitData, proof, device: int = 0) -> bool:
+    """checkCombinedPlonkEquations' (Plonk/Verifier.hs:35-51): the quotient identity
+    Q_i(zeta) (zeta^n - 1) == C_i(zeta) for every challenge round (eqs_ok of verifyProof)."""
+    inf = vkey.info
+    tr, o = _trace_one(vkey, proof, device), trace_offsets(inf.num_challenges, inf.num_fri_steps, inf.num_query_rounds)
+    return bool(int(tr[o["flags"]]) & 1)
+
+
 def _status_to_bool(st: int) -> bool:
     if st == ACCEPT:
         return True
