@@ -5,6 +5,7 @@
  *
  *   p2v_verify [--pack-only] [--devices N] [--dump FILE] common.json vkey.json proof.json [proof.json ...]
  *   p2v_verify --words [...] circuit.words proof.words [proof.words ...]
+ *   p2v_verify --bytes [...] common.json vkey.json proof.bin [proof.bin ...]
  *
  * Prints one line per proof, "<file> <status>": 1 True, 0 False, < 0 the class of `error`
  * the reference would raise (include/p2v.h).  With --pack-only the proofs are decoded and
@@ -12,7 +13,9 @@
  * --devices N shards the batch over devices 0..N-1 (p2v_verify_batch_devices).
  * --words: the inputs are the word-encoded Types.hs values (little-endian u64 files, the
  * layout of include/p2v.h that a typed host such as the Haskell shim writes) instead of JSON:
- * p2v_circuit_from_words + p2v_pack_proof_words.  --dump FILE writes the packed words.
+ * p2v_circuit_from_words + p2v_pack_proof_words.  --bytes: the proofs are plonky2's binary
+ * serialization (p2v_pack_proof_bytes).  --ext FLAGS: opt-in plonky2 conventions (P2V_EXT_*,
+ * p2v_circuit_from_*_ex).  --dump FILE writes the packed words.
  * Exit: 0 done, 2 usage / IO, 3 circuit rejected, 4 a proof did not decode, 5 device error.
  *
  * Build: gcc -O2 -I include examples/p2v_verify.c -L plonky2-verifier_amd -lp2v \
@@ -39,19 +42,23 @@ static char* read_file(const char* path, size_t* len) {
 }
 
 int main(int argc, char** argv) {
-  int pack_only = 0, ndev = 1, a = 1, wordsin = 0;
+  int pack_only = 0, ndev = 1, a = 1, wordsin = 0, bytesin = 0;
+  uint32_t ext = 0;
   const char* dump = NULL;
   for (; a < argc && argv[a][0] == '-' && argv[a][1] == '-'; a++) {
     if (!strcmp(argv[a], "--pack-only")) pack_only = 1;
     else if (!strcmp(argv[a], "--words")) wordsin = 1;
+    else if (!strcmp(argv[a], "--bytes")) bytesin = 1;
+    else if (!strcmp(argv[a], "--ext") && a + 1 < argc) ext = (uint32_t)strtoul(argv[++a], NULL, 0);
     else if (!strcmp(argv[a], "--devices") && a + 1 < argc) ndev = atoi(argv[++a]);
     else if (!strcmp(argv[a], "--dump") && a + 1 < argc) dump = argv[++a];
     else { fprintf(stderr, "unknown option %s\n", argv[a]); return 2; }
   }
   const int nhdr = wordsin ? 1 : 2;   /* circuit.words | common.json vkey.json */
-  if (argc - a < nhdr + 1 || ndev < 1) {
-    fprintf(stderr, "usage: %s [--pack-only] [--devices N] [--dump FILE] common.json vkey.json proof.json...\n"
-                    "       %s --words [...] circuit.words proof.words...\n", argv[0], argv[0]);
+  if (argc - a < nhdr + 1 || ndev < 1 || (wordsin && bytesin)) {
+    fprintf(stderr, "usage: %s [--pack-only] [--devices N] [--dump FILE] [--ext FLAGS] common.json vkey.json proof.json...\n"
+                    "       %s --words [...] circuit.words proof.words...\n"
+                    "       %s --bytes [...] common.json vkey.json proof.bin...\n", argv[0], argv[0], argv[0]);
     return 2;
   }
   size_t clen = 0, vlen = 0;
@@ -59,8 +66,8 @@ int main(int argc, char** argv) {
   char* vkey = wordsin ? NULL : read_file(argv[a + 1], &vlen);
   if (!common || (!wordsin && !vkey)) { fprintf(stderr, "cannot read the circuit files\n"); return 2; }
   p2v_circuit* circ = NULL;
-  int crc = wordsin ? p2v_circuit_from_words((const uint64_t*)common, clen / 8, &circ)
-                    : p2v_circuit_from_json(common, clen, vkey, vlen, &circ);
+  int crc = wordsin ? p2v_circuit_from_words_ex((const uint64_t*)common, clen / 8, ext, &circ)
+                    : p2v_circuit_from_json_ex(common, clen, vkey, vlen, ext, &circ);
   if (crc != P2V_OK) {
     fprintf(stderr, "circuit: %s\n", p2v_last_error_message());
     return 3;
@@ -76,9 +83,12 @@ int main(int argc, char** argv) {
   }
   uint64_t* words = (uint64_t*)malloc((size_t)n * (size_t)info.proof_words * sizeof(uint64_t));
   int32_t* codes = (int32_t*)malloc((size_t)n * sizeof(int32_t));
-  if (wordsin) {
+  if (wordsin || bytesin) {
     for (int i = 0; i < n; i++) {
-      if (p2v_pack_proof_words(circ, (const uint64_t*)texts[i], lens[i] / 8, words + (size_t)i * (size_t)info.proof_words) != P2V_OK) {
+      uint64_t* dst = words + (size_t)i * (size_t)info.proof_words;
+      const int rc = wordsin ? p2v_pack_proof_words(circ, (const uint64_t*)texts[i], lens[i] / 8, dst)
+                             : p2v_pack_proof_bytes(circ, (const uint8_t*)texts[i], lens[i], dst);
+      if (rc != P2V_OK) {
         fprintf(stderr, "%s: %s\n", argv[a + nhdr + i], p2v_last_error_message());
         return 4;
       }

@@ -81,3 +81,33 @@ def test_bytes_fuzz_never_crashes():
             assert e.code in (p2v.E_PARSE, p2v.E_SHAPE), e
             seen.add(e.code)
     assert {p2v.E_PARSE, p2v.E_SHAPE} <= seen
+
+
+def test_c_host_bytes_mode_equals_json_mode(tmp_path):
+    """examples/p2v_verify.c --bytes (plonky2 binary proofs, p2v_pack_proof_bytes) with --ext 7 (the
+    P2V_EXT_* conventions through p2v_circuit_from_json_ex) packs the same words as the JSON mode."""
+    import os
+    import subprocess
+    p2v = p2v_module()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "plonky2-verifier_amd", "p2v_verify")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(root, "plonky2-verifier_amd"), "p2v_verify"])
+    gc = gen_circuit(6, 4, 0, 1, 28, 8, 0, 1, 7, (3, 2))
+    (tmp_path / "c.json").write_bytes(gc.common)
+    (tmp_path / "v.json").write_bytes(gc.vkey)
+    js, bs = [], []
+    for i, pr in enumerate([gc.proof(1, 1), gc.proof(2, 2)]):
+        (tmp_path / f"p{i}.json").write_bytes(pr)
+        (tmp_path / f"p{i}.bin").write_bytes(proof_bytes(pr, pi_prefix=bool(i)))
+        js.append(str(tmp_path / f"p{i}.json"))
+        bs.append(str(tmp_path / f"p{i}.bin"))
+    hdr = [str(tmp_path / "c.json"), str(tmp_path / "v.json")]
+    a = subprocess.run([exe, "--ext", "7", "--pack-only", "--dump", str(tmp_path / "a.out")] + hdr + js, capture_output=True, text=True)
+    b = subprocess.run([exe, "--bytes", "--ext", "7", "--pack-only", "--dump", str(tmp_path / "b.out")] + hdr + bs,
+                       capture_output=True, text=True)
+    assert a.returncode == 0 and b.returncode == 0, (a.stderr, b.stderr)
+    da, db = np.fromfile(tmp_path / "a.out", np.uint64), np.fromfile(tmp_path / "b.out", np.uint64)
+    assert da.size == 2 * p2v.VerifierCircuitData.from_json(gc.common, gc.vkey, 7).info.proof_words
+    assert np.array_equal(da, db)
+    # without the flags the MinSize circuit is the reference's circuit error (exit 3)
+    assert subprocess.run([exe, "--pack-only"] + hdr + js, capture_output=True).returncode == 3
