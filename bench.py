@@ -397,7 +397,17 @@ def main():
     import torch
     import torch.distributed as dist
     if world > 1:
-        dist.init_process_group(args.dist_backend if torch.cuda.is_available() else "gloo")
+        # stdout carries exactly one JSON line: the backends' own start-up chatter (gloo prints
+        # its peer count to fd 1) goes to stderr
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(args.dist_backend if torch.cuda.is_available() else "gloo")
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     # one rank per GPU; ranks beyond the visible GPUs (gloo rehearsal only) share devices
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
