@@ -237,6 +237,18 @@ int  p2v_verifier_run_json(p2v_verifier* v, const char* blob, const uint64_t* of
 int  p2v_verifier_pack_json(p2v_verifier* v, const char* blob, const uint64_t* offsets, size_t n,
                             int32_t* codes, size_t* n_device, uint64_t* words, void* stream);
 
+/* plonky2 binary proofs on the GPU: proof i is blob[offsets[i] .. offsets[i+1]) in the format of
+ * p2v_pack_proof_bytes.  For a given circuit that format is a fixed map of byte offsets, so the
+ * texts are copied to the device and packed there by one workgroup per proof (json_pack.hip
+ * k_bytes_pack); a proof that fails a length / sibling-count / public-input check is packed by the
+ * host reader instead, so words and codes (P2V_OK / P2V_E_PARSE / P2V_E_SHAPE) always equal
+ * p2v_pack_proof_bytes.  n_device (optional) receives how many proofs the device packed.  run:
+ * then verified (results as p2v_verifier_run_json); pack: the packed words copied to `words`. */
+int  p2v_verifier_run_bytes(p2v_verifier* v, const uint8_t* blob, const uint64_t* offsets, size_t n,
+                            int8_t* results, int32_t* codes, size_t* n_device, void* stream);
+int  p2v_verifier_pack_bytes(p2v_verifier* v, const uint8_t* blob, const uint64_t* offsets, size_t n,
+                             int32_t* codes, size_t* n_device, uint64_t* words, void* stream);
+
 /* One-shot convenience: create a verifier on `device`, verify, free. */
 int  p2v_verify_batch(const p2v_circuit* c, const uint64_t* proofs, size_t n,
                       int8_t* results, int device);

@@ -31,6 +31,8 @@ extern "C" __global__ void k_vanish_final(DevCircuit);
 extern "C" __global__ void k_status(DevCircuit, int8_t*, uint64_t*, int64_t);
 extern "C" __global__ void k_selftest(int, const uint64_t*, const uint64_t*, uint64_t*, int64_t);
 extern "C" __global__ void k_json_pack(const uint8_t*, const uint64_t*, int, const uint8_t*, int64_t, const int32_t*, int64_t, uint64_t*, int64_t, int8_t*);
+extern "C" __global__ void k_bytes_pack(const uint8_t*, const uint64_t*, int, const int64_t*, const int64_t*, const int64_t*, int,
+                                        const int64_t*, const uint8_t*, int, int64_t, int64_t, int64_t, uint64_t*, int64_t, int8_t*);
 
 using namespace p2v;
 
@@ -92,6 +94,11 @@ struct p2v_verifier {
   bool have_tmpl = false;
   int64_t skel_len = 0, ntok = 0;
   DevBuf j_blob, j_offs, j_skel, j_tok, j_ok;
+  // binary-proof ingest (p2v_verifier_run_bytes): the circuit's byte map on the device, made once
+  DevBuf b_rsrc, b_rdst, b_rlen, b_coff, b_cval;
+  bool have_bmap = false;
+  int nruns = 0, nchk = 0;
+  int64_t bfixed = 0;
   // pinned host staging for the small device->host results (statuses, JSON ok flags): a copy
   // to pageable memory would stage through the runtime and stall the other streams' work
   int8_t* h_res = nullptr;
@@ -247,7 +254,8 @@ void p2v_verifier_free(p2v_verifier* v) {
   if (!v) return;
   (void)hipSetDevice(v->device);
   for (DevBuf* b : {&v->in, &v->soa, &v->chal, &v->leafdig, &v->mk, &v->fbits, &v->qvals, &v->van, &v->vparts, &v->lutre, &v->res, &v->trace, &v->t_cs, &v->t_kis,
-                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit, &v->t_rin, &v->t_rout, &v->t_roff, &v->t_rch, &v->t_pbase, &v->lutpart, &v->j_blob, &v->j_offs, &v->j_skel, &v->j_tok, &v->j_ok})
+                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit, &v->t_rin, &v->t_rout, &v->t_roff, &v->t_rch, &v->t_pbase, &v->lutpart, &v->j_blob, &v->j_offs, &v->j_skel, &v->j_tok, &v->j_ok,
+                    &v->b_rsrc, &v->b_rdst, &v->b_rlen, &v->b_coff, &v->b_cval})
     b->free_();
   if (v->timed) for (auto& e : v->ev) (void)hipEventDestroy(e);
   if (v->dep_p1) (void)hipEventDestroy(v->dep_p1);
@@ -701,6 +709,88 @@ static int pack_json_into(p2v_verifier* v, const char* blob, const uint64_t* off
     } catch (const ShapeError&) { codes[i] = P2V_E_SHAPE; }
     catch (...) { codes[i] = P2V_E_PARSE; }
   }
+  return P2V_OK;
+}
+
+// plonky2 binary proofs -> packed rows of v->in (k_bytes_pack against the circuit's byte map,
+// the host reader for any proof that fails a check); codes[i] as p2v_pack_proof_bytes
+static int pack_bytes_into(p2v_verifier* v, const uint8_t* blob, const uint64_t* offsets, size_t n,
+                           int32_t* codes, size_t* n_device, void* stream_) {
+  if (n_device) *n_device = 0;
+  if (!v || (n && (!blob || !offsets || !codes))) return fail(P2V_E_ARG, "null argument");
+  if (n > v->max_batch) return fail(P2V_E_ARG, "batch larger than max_batch");
+  if (n == 0) return P2V_OK;
+  HCK(hipSetDevice(v->device));
+  hipStream_t st = (hipStream_t)stream_;
+  const Circuit& C = v->circ->c;
+  const int64_t W = C.L.words;
+  if (!v->have_bmap) {
+    const BytesMap m = bytes_map(C);
+    auto put = [&](DevBuf& b, const void* h, size_t bytes) -> hipError_t {
+      hipError_t e = b.alloc(bytes + 16);
+      if (e == hipSuccess && bytes) e = hipMemcpy(b.p, h, bytes, hipMemcpyHostToDevice);
+      return e;
+    };
+    HCK(put(v->b_rsrc, m.run_src.data(), m.run_src.size() * 8));
+    HCK(put(v->b_rdst, m.run_dst.data(), m.run_dst.size() * 8));
+    HCK(put(v->b_rlen, m.run_len.data(), m.run_len.size() * 8));
+    HCK(put(v->b_coff, m.chk_off.data(), m.chk_off.size() * 8));
+    HCK(put(v->b_cval, m.chk_val.data(), m.chk_val.size()));
+    v->nruns = (int)m.run_len.size(); v->nchk = (int)m.chk_off.size(); v->bfixed = m.fixed;
+    v->have_bmap = true;
+  }
+  const uint64_t base = offsets[0], bytes = offsets[n] - base;
+  if (v->j_blob.bytes < bytes + 64) { v->j_blob.free_(); HCK(v->j_blob.alloc(bytes + 64)); }   // + unaligned-load slack
+  if (v->j_offs.bytes < (n + 1) * 8) { v->j_offs.free_(); HCK(v->j_offs.alloc((n + 1) * 8)); }
+  if (v->j_ok.bytes < n) { v->j_ok.free_(); HCK(v->j_ok.alloc(n)); }
+  std::vector<uint64_t> rel(n + 1);
+  for (size_t i = 0; i <= n; i++) rel[i] = offsets[i] - base;
+  HCK(hipMemcpyAsync(v->j_blob.p, blob + base, bytes, hipMemcpyHostToDevice, st));
+  HCK(hipMemcpyAsync(v->j_offs.p, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, st));
+  k_bytes_pack<<<(unsigned)n, 256, 0, st>>>((const uint8_t*)v->j_blob.p, (const uint64_t*)v->j_offs.p, (int)n, (const int64_t*)v->b_rsrc.p,
+                                            (const int64_t*)v->b_rdst.p, (const int64_t*)v->b_rlen.p, v->nruns, (const int64_t*)v->b_coff.p,
+                                            (const uint8_t*)v->b_cval.p, v->nchk, v->bfixed, (int64_t)C.num_pis, C.L.pis,
+                                            (uint64_t*)v->in.p, W, (int8_t*)v->j_ok.p);
+  HCK(hipGetLastError());
+  HCK(hipMemcpyAsync(v->h_res, v->j_ok.p, n, hipMemcpyDeviceToHost, st));
+  HCK(hipStreamSynchronize(st));
+  std::vector<int8_t> okf(v->h_res, v->h_res + n);
+  std::vector<uint64_t> row((size_t)W);
+  for (size_t i = 0; i < n; i++) {
+    codes[i] = P2V_OK;
+    if (okf[i]) { if (n_device) (*n_device)++; continue; }
+    try {
+      pack_proof_bytes(C, blob + offsets[i], (size_t)(offsets[i + 1] - offsets[i]), row.data());
+      HCK(hipMemcpyAsync((uint64_t*)v->in.p + i * W, row.data(), (size_t)W * 8, hipMemcpyHostToDevice, st));
+      HCK(hipStreamSynchronize(st));   // row is reused
+    } catch (const ShapeError&) { codes[i] = P2V_E_SHAPE; }
+    catch (...) { codes[i] = P2V_E_PARSE; }
+  }
+  return P2V_OK;
+}
+
+int p2v_verifier_pack_bytes(p2v_verifier* v, const uint8_t* blob, const uint64_t* offsets, size_t n,
+                            int32_t* codes, size_t* n_device, uint64_t* words, void* stream_) {
+  int rc = pack_bytes_into(v, blob, offsets, n, codes, n_device, stream_);
+  if (rc != P2V_OK || n == 0 || !words) return rc;
+  hipStream_t st = (hipStream_t)stream_;
+  const size_t W = (size_t)v->circ->c.L.words;
+  HCK(hipMemcpyAsync(words, v->in.p, n * W * 8, hipMemcpyDeviceToHost, st));
+  HCK(hipStreamSynchronize(st));
+  for (size_t i = 0; i < n; i++)
+    if (codes[i] != P2V_OK) memset(words + i * W, 0, W * 8);
+  return P2V_OK;
+}
+
+int p2v_verifier_run_bytes(p2v_verifier* v, const uint8_t* blob, const uint64_t* offsets, size_t n,
+                           int8_t* results, int32_t* codes, size_t* n_device, void* stream_) {
+  if (n && !results) return fail(P2V_E_ARG, "null argument");
+  int rc = pack_bytes_into(v, blob, offsets, n, codes, n_device, stream_);
+  if (rc != P2V_OK || n == 0) return rc;
+  rc = p2v_verifier_run(v, (const uint64_t*)v->in.p, n, results, nullptr, stream_, P2V_FLAG_INPUT_DEVICE);
+  if (rc != P2V_OK) return rc;
+  for (size_t i = 0; i < n; i++)
+    if (codes[i] != P2V_OK) results[i] = codes[i] == P2V_E_SHAPE ? P2V_ERR_SHAPE : P2V_ERR_PARSE;
   return P2V_OK;
 }
 

@@ -636,17 +636,15 @@ struct ByteReader {
 };
 }  // namespace
 
-void pack_proof_bytes(const Circuit& C, const uint8_t* bytes, size_t n, uint64_t* dst) {
+// The fixed part of the format in order: fields(dst_word, nwords, what) for every run of u64
+// words, count(expected, what) for every u8 sibling count.  Shared by the host reader below and
+// the device packer's map (bytes_map), so both follow one order.
+template <class Fields, class Count>
+static void bytes_walk(const Circuit& C, Fields&& fields, Count&& count) {
   const Layout& L = C.L;
-  ByteReader R{bytes, n};
-  auto fields = [&](int64_t off, int64_t k, const char* what) { for (int64_t i = 0; i < k; i++) dst[off + i] = R.u64(what) % gl::P; };
   auto exts = [&](int64_t off, int64_t k, const char* what) { fields(off, 2 * k, what); };
   auto cap = [&](int64_t off, const char* what) { fields(off, 4 * (int64_t)C.cap_len, what); };
-  auto path = [&](int64_t off, int depth, const char* what) {
-    const int len = R.u8(what);
-    if (len != depth) throw ShapeError(std::string(what) + ": expected " + std::to_string(depth) + " siblings, got " + std::to_string(len));
-    fields(off, 4 * (int64_t)depth, what);
-  };
+  auto path = [&](int64_t off, int depth, const char* what) { count(depth, what); fields(off, 4 * (int64_t)depth, what); };
   cap(L.wcap, "wires_cap");
   cap(L.zcap, "plonk_zs_partial_products_cap");
   cap(L.qcap, "quotient_polys_cap");
@@ -673,7 +671,18 @@ void pack_proof_bytes(const Circuit& C, const uint8_t* bytes, size_t n, uint64_t
     }
   }
   exts(L.final_poly, C.final_len, "final_poly.coeffs");
-  dst[L.pow] = R.u64("pow_witness") % gl::P;
+  fields(L.pow, 1, "pow_witness");
+}
+
+void pack_proof_bytes(const Circuit& C, const uint8_t* bytes, size_t n, uint64_t* dst) {
+  const Layout& L = C.L;
+  ByteReader R{bytes, n};
+  auto fields = [&](int64_t off, int64_t k, const char* what) { for (int64_t i = 0; i < k; i++) dst[off + i] = R.u64(what) % gl::P; };
+  auto count = [&](int depth, const char* what) {
+    const int len = R.u8(what);
+    if (len != depth) throw ShapeError(std::string(what) + ": expected " + std::to_string(depth) + " siblings, got " + std::to_string(len));
+  };
+  bytes_walk(C, fields, count);
   const size_t rest = n - R.i, np = (size_t)C.num_pis;
   if (rest == 8 * np) fields(L.pis, C.num_pis, "public_inputs");
   else if (rest == 8 * (np + 1)) {
@@ -682,6 +691,22 @@ void pack_proof_bytes(const Circuit& C, const uint8_t* bytes, size_t n, uint64_t
   } else {
     throw ShapeError("public_inputs: " + std::to_string(rest) + " trailing bytes for " + std::to_string(np) + " public inputs");
   }
+}
+
+BytesMap bytes_map(const Circuit& C) {
+  BytesMap m;
+  int64_t pos = 0;
+  auto fields = [&](int64_t off, int64_t k, const char*) {
+    if (k <= 0) return;
+    const size_t r = m.run_len.size();
+    if (r && m.run_src[r - 1] + 8 * m.run_len[r - 1] == pos && m.run_dst[r - 1] + m.run_len[r - 1] == off) m.run_len[r - 1] += k;
+    else { m.run_src.push_back(pos); m.run_dst.push_back(off); m.run_len.push_back(k); }
+    pos += 8 * k;
+  };
+  auto count = [&](int depth, const char*) { m.chk_off.push_back(pos); m.chk_val.push_back((uint8_t)depth); pos += 1; };
+  bytes_walk(C, fields, count);
+  m.fixed = pos;
+  return m;
 }
 
 // ------------------------------------------------------------------ template-guided pack

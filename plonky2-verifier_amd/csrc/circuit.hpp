@@ -78,6 +78,16 @@ Circuit parse_circuit_words(const uint64_t* words, size_t n, uint32_t ext = 0); 
 void pack_proof_words(const Circuit& c, const uint64_t* words, size_t n, uint64_t* dst);   // ParseError / ShapeError
 // plonky2's binary ProofWithPublicInputs serialization (circuit.cpp); ParseError / ShapeError
 void pack_proof_bytes(const Circuit& c, const uint8_t* bytes, size_t n, uint64_t* dst);
+// The same format as a fixed map for the device packer (json_pack.hip k_bytes_pack): runs of u64
+// words (source byte offset, packed word, count) in file order, the sibling-count bytes and their
+// expected values, and the byte length before the public inputs.
+struct BytesMap {
+  std::vector<int64_t> run_src, run_dst, run_len;
+  std::vector<int64_t> chk_off;
+  std::vector<uint8_t> chk_val;
+  int64_t fixed = 0;
+};
+BytesMap bytes_map(const Circuit& c);
 // throws ParseError / ShapeError; rec (optional, [words]) receives each packed word's number ordinal
 void pack_proof(const Circuit& c, const JVal& proof, uint64_t* dst, int32_t* rec = nullptr);
 

@@ -163,3 +163,55 @@ extern "C" __global__ void __launch_bounds__(256) k_json_pack(const uint8_t* __r
   __syncthreads();
   if (t == 0) okf[p] = s_bad ? 0 : 1;
 }
+
+// ------------------------------------------------------------------ plonky2 binary proofs
+// plonky2's byte serialization (circuit.cpp pack_proof_bytes) has a fixed layout for a given
+// circuit: runs of little-endian u64 words at fixed byte offsets, u8 sibling counts at fixed
+// offsets, then the public inputs (raw, or after a u64 count).  The host turns it into a map
+// (circuit.cpp bytes_map: runs of (source byte, packed word, count), count bytes and their values);
+// one workgroup per proof checks the length, the count bytes and the PI form, then copies every
+// run into the packed row with coalesced loads and stores, reducing mod p.  A proof that fails
+// any check is flagged and packed by the host reader (the exact error code).  Words after a count
+// byte sit at odd byte offsets: each is assembled from three aligned dwords with v_alignbyte
+// (the blob has 64 bytes of slack past its end).
+__device__ __forceinline__ uint64_t ld_u64_any(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
+  const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t modp(uint64_t x) { return x >= gl::P ? x - gl::P : x; }
+
+extern "C" __global__ void __launch_bounds__(256) k_bytes_pack(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs, int n,
+                                                               const int64_t* __restrict__ rsrc, const int64_t* __restrict__ rdst,
+                                                               const int64_t* __restrict__ rlen, int nruns,
+                                                               const int64_t* __restrict__ coff, const uint8_t* __restrict__ cval, int nchk,
+                                                               int64_t fixed, int64_t npis, int64_t pis_dst,
+                                                               uint64_t* __restrict__ dst, int64_t W, int8_t* __restrict__ ok) {
+  const int i = blockIdx.x;
+  if (i >= n) return;
+  const uint8_t* s = blob + offs[i];
+  const int64_t L = (int64_t)(offs[i + 1] - offs[i]);
+  int64_t pis_src = -1;
+  if (L == fixed + 8 * npis) pis_src = fixed;
+  else if (L == fixed + 8 + 8 * npis && ld_u64_any(s + fixed) == (uint64_t)npis) pis_src = fixed + 8;
+  int good = pis_src >= 0;
+  if (good)
+    for (int k = threadIdx.x; k < nchk; k += blockDim.x) good &= s[coff[k]] == cval[k];
+  good = __syncthreads_and(good);
+  if (!good) {
+    if (threadIdx.x == 0) ok[i] = 0;
+    return;
+  }
+  uint64_t* d = dst + (int64_t)i * W;
+  for (int r = 0; r < nruns; r++) {
+    const uint8_t* src = s + rsrc[r];
+    uint64_t* out = d + rdst[r];
+    const int64_t len = rlen[r];
+    for (int64_t k = threadIdx.x; k < len; k += blockDim.x) out[k] = modp(ld_u64_any(src + 8 * k));
+  }
+  for (int64_t k = threadIdx.x; k < npis; k += blockDim.x) d[pis_dst + k] = modp(ld_u64_any(s + pis_src + 8 * k));
+  if (threadIdx.x == 0) ok[i] = 1;
+}

@@ -130,6 +130,8 @@ def lib() -> ctypes.CDLL:
     L.p2v_verifier_run.argtypes = [vp, u64p, sz, i8p, u64p, vp, ctypes.c_uint32]
     L.p2v_verifier_run_json.argtypes = [vp, vp, vp, sz, i8p, vp, vp, vp]
     L.p2v_verifier_pack_json.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp]
+    L.p2v_verifier_run_bytes.argtypes = [vp, vp, vp, sz, i8p, vp, vp, vp]
+    L.p2v_verifier_pack_bytes.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp]
     L.p2v_verify_batch.argtypes = [vp, u64p, sz, i8p, ctypes.c_int]
     L.p2v_verify_batch_devices.argtypes = [vp, u64p, sz, i8p, ctypes.POINTER(ctypes.c_int), ctypes.c_int, sz]
     L.p2v_verifier_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
@@ -346,6 +348,33 @@ class BatchVerifier:
         _check(lib().p2v_verifier_pack_json(self._h, blob.ctypes.data, offs.ctypes.data, n, codes.ctypes.data,
                                             ctypes.addressof(ndev), words.ctypes.data, ctypes.c_void_p(stream)))
         self.last_json_device = ndev.value
+        return words, codes
+
+    def run_bytes(self, proofs: Union[Sequence[bytes], tuple], stream: int = 0):
+        """plonky2 binary proofs (p2v_pack_proof_bytes' format) -> (int8 statuses, int32 decode
+        codes) via p2v_verifier_run_bytes (copied to the device and packed there).  Same inputs as
+        run_json; the device-packed count is left in `self.last_bytes_device`."""
+        blob, offs = self._json_batch(proofs)
+        n = offs.size - 1
+        res = np.empty(n, dtype=np.int8)
+        codes = np.empty(n, dtype=np.int32)
+        ndev = ctypes.c_size_t(0)
+        _check(lib().p2v_verifier_run_bytes(self._h, blob.ctypes.data, offs.ctypes.data, n, res.ctypes.data, codes.ctypes.data,
+                                            ctypes.addressof(ndev), ctypes.c_void_p(stream)))
+        self.last_bytes_device = ndev.value
+        return res, codes
+
+    def pack_bytes(self, proofs: Union[Sequence[bytes], tuple], stream: int = 0):
+        """plonky2 binary proofs -> (uint64 [n, proof_words] packed words, int32 decode codes),
+        packed on the device (p2v_verifier_pack_bytes)."""
+        blob, offs = self._json_batch(proofs)
+        n = offs.size - 1
+        words = np.empty((n, self.circuit.info.proof_words), dtype=np.uint64)
+        codes = np.empty(n, dtype=np.int32)
+        ndev = ctypes.c_size_t(0)
+        _check(lib().p2v_verifier_pack_bytes(self._h, blob.ctypes.data, offs.ctypes.data, n, codes.ctypes.data,
+                                             ctypes.addressof(ndev), words.ctypes.data, ctypes.c_void_p(stream)))
+        self.last_bytes_device = ndev.value
         return words, codes
 
     def run_device(self, proofs_ptr: int, n: int, results_ptr: int, stream: int = 0, trace_ptr: int = 0,

@@ -243,6 +243,43 @@ def test_gpu_random_number_mutations_vs_oracle(p2v, nb, mode, lk):
     assert len(set(sts)) >= 3   # the campaign reaches several outcome classes
 
 
+@pytest.mark.parametrize("args,ext", [((6, 4, 0, 1, 28, 16, 0, 1), 0), ((6, 0, 1, 1, 28, 16), 0),
+                                      ((6, 4, 0, 1, 28, 16, 0, 1, 7, (3, 2)), 7)])
+def test_gpu_bytes_ingest_matches_host_reader(p2v, args, ext):
+    """Binary proofs packed on the GPU (k_bytes_pack, p2v_verifier_pack_bytes / run_bytes): words,
+    codes and statuses equal the host reader's (p2v_pack_proof_bytes) and the JSON path's, for both
+    public-input forms, on a batch with malformed proofs (truncated, a wrong sibling count,
+    trailing bytes) that must fall back to the host reader with its exact error."""
+    from support import proof_bytes
+    gc = gen_circuit(*args)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey, ext)
+    texts = [gc.proof(1, 1), gc.proof(2, 2), gc.proof(1, 3, flags=1), gc.proof(1, 4, flags=2)]
+    bins = [proof_bytes(t, pi_prefix=bool(i % 2)) for i, t in enumerate(texts)]
+    bad = [bins[0][: len(bins[0]) // 3], bins[1] + b"\0" * 8, bytearray(bins[2])]
+    cap_bytes = 32 * (1 << vk.info.cap_height)
+    i = 3 * cap_bytes + 16 * (vk.info.num_openings_this + vk.info.num_openings_next)   # the first sibling count
+    i += cap_bytes * vk.info.num_fri_steps + 8 * vk.info.leaf_widths[0]
+    bad[2][i] += 1
+    batch = bins * 8 + [bytes(b) for b in bad]
+    bv = p2v.BatchVerifier(vk, 0, len(batch))
+    words, codes = bv.pack_bytes(batch)
+    assert bv.last_bytes_device == len(bins) * 8
+    for k, b in enumerate(batch):
+        try:
+            ref, code = vk.pack_bytes(b), 0
+        except p2v.P2VError as e:
+            ref, code = None, e.code
+        assert codes[k] == code, k
+        if ref is not None:
+            assert np.array_equal(words[k], ref), k
+    assert list(codes[-3:]) == [p2v.E_PARSE, p2v.E_SHAPE, p2v.E_SHAPE]
+    res, codes2 = bv.run_bytes(batch)
+    assert np.array_equal(codes2, codes)
+    ref_res = bv.run(vk.pack_many(texts))
+    assert np.array_equal(res[: len(bins) * 8], np.tile(ref_res, 8))
+    assert list(res[-3:]) == [-7, -5, -5]
+
+
 def test_gpu_reference_intermediates(p2v):
     """proof_challenges / eval_combined_plonk_constraints / check_combined_plonk_equations (the
     sub-results src/testmain.hs:54-63 prints) equal the oracle's trace words; the identity
