@@ -1,0 +1,9 @@
+#!/bin/bash
+# the whole GPU suite on the current tree (what the driver runs at round end)
+set -e
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r02_probe12
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+echo done
