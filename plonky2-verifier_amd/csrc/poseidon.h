@@ -174,7 +174,9 @@ namespace dv {
 // acc + C a as one v_mad_u64_u32 with the matrix entry C as an inline constant.  The carry-out
 // is never needed: it goes to a fixed, clobbered SGPR pair rather than an asm output (an asm
 // SGPR output costs a wait state before every consumer, and the compiler would turn C = 2, 16
-// into 64-bit shifts of zero-extended register pairs).
+// into 64-bit shifts of zero-extended register pairs).  The pair must lie inside the kernel's
+// SGPR budget: a build that forces a higher occupancy (e.g. amdgpu_waves_per_eu(7) on k_merkle)
+// makes hipcc warn "clobber list contains reserved registers: s94, s95", and is not valid.
 template <uint32_t C>
 __device__ __forceinline__ uint64_t madk(uint32_t a, uint64_t acc) {
   uint64_t d;
