@@ -565,7 +565,8 @@ def main():
                          "traffic_bytes_per_launch": traffic_bytes, "algorithmic_bytes_per_launch": kb[dom] * B,
                          "note": "integer-VALU bound (Poseidon); HBM fraction reported as the metric asks"},
             "valu": {"perms_per_proof": ppp, "perm_rate_G": round(value / world * ppp / 1e9, 3),
-                     "issue": valu_roofline(kavg, dt / args.steps * 1e3, B) if not args.lookups else None},
+                     "issue": valu_roofline(kavg, dt / args.steps * 1e3, B)
+                     if (real and info.degree_bits == 12 and not args.lookups) else None},   # the PMC pass's own workload only
             "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
             "verified_all": ok,
         }
