@@ -88,13 +88,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_workload(degree_bits, distinct, witnesses, seed_base, threads, lookups=0, real=False):
+def make_workload(degree_bits, distinct, witnesses, seed_base, threads, lookups=0, real=False, ext=0, arities=()):
     """real: the generator's real circuit (every gate of the recursion set on rows, selector
     polynomials, copy constraints, a genuine quotient: every vanishing term non-zero at zeta);
-    else the degenerate circuit (same shapes and the same verifier work, gate filters 0)."""
+    else the degenerate circuit (same shapes and the same verifier work, gate filters 0).
+    ext / arities: the opt-in plonky2 conventions (P2V_EXT_*; arities under MinSize or Fixed)."""
     from support import generator
     g = generator()
-    gc = g.circuit(degree_bits, 4, lookups, 1, 28, 16, 0, 1 if real else 0)
+    gc = g.circuit(degree_bits, 4, lookups, 1, 28, 16, 0, 1 if real else 0, ext, tuple(arities))
     wseeds = [seed_base * 1000 + i + 1 for i in range(witnesses)]
     with cf.ThreadPoolExecutor(threads) as ex:
         list(ex.map(gc.witness, wseeds))
@@ -108,7 +109,7 @@ def kernel_bytes_model(info, trace_words):
     packed layout: the bytes the algorithm must move, not what it does."""
     W = info.proof_words
     Q, S, r = info.num_query_rounds, info.num_fri_steps, info.num_challenges
-    widths = sum(info.oracle_widths)
+    widths = sum(info.leaf_widths)
     step_evals = sum(2 << a for a in info.step_arity_bits)
     depth0 = info.lde_bits - info.cap_height
     step_depths, logn = [], info.lde_bits
@@ -141,7 +142,7 @@ def mutate_batch(rows, info, every=16):
     P = 0xFFFFFFFF00000001
     W, Q = info.proof_words, info.num_query_rounds
     depth0 = info.lde_bits - info.cap_height
-    qstride = sum(info.oracle_widths) + 4 * 4 * depth0
+    qstride = sum(info.leaf_widths) + 4 * 4 * depth0
     logn = info.lde_bits
     for a in info.step_arity_bits:
         logn -= a
@@ -158,7 +159,9 @@ def mutate_batch(rows, info, every=16):
 def perms_per_proof(info, num_pis=4):
     """Poseidon permutations per proof (SURVEY.md §8d model; commentary/FRI.md:263-265)."""
     Q = info.num_query_rounds
-    leaf = sum((w + 7) // 8 for w in info.oracle_widths) + sum(((2 << a) + 7) // 8 for a in info.step_arity_bits)
+    noop = bool(info.ext & 4)   # P2V_EXT_HASH_OR_NOOP: leaves of <= 4 elements are not hashed
+    sponge = lambda w: 0 if noop and w <= 4 else (w + 7) // 8   # noqa: E731
+    leaf = sum(sponge(w) for w in info.leaf_widths) + sum(sponge(2 << a) for a in info.step_arity_bits)
     depth0 = info.lde_bits - info.cap_height
     paths, logn = 4 * depth0, info.lde_bits
     for a in info.step_arity_bits:
@@ -410,6 +413,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=2, help="batches in flight per GPU (workspaces/streams)")
     ap.add_argument("--layout", choices=("tiled", "proof-major"), default="tiled",
                     help="device-resident batch layout: 64-proof tiles (P2V_FLAG_INPUT_TILED, coalesced loads) or proof-major rows")
+    ap.add_argument("--ext", type=int, default=0, help="P2V_EXT_* flags of the workload circuit (1 MinSize arities, 2 hiding, 4 hash_or_noop)")
+    ap.add_argument("--arities", default="", help="comma-separated FRI arity bits (with --ext 1: MinSize; else Fixed)")
     ap.add_argument("--lookups", type=int, default=0,
                     help="0: standard recursion circuit (C2); 2: + LookupGate/LookupTableGate with a 256-entry and a 2^16-entry table (C3 circuit)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -461,9 +466,10 @@ def main():
     threads = max(1, min(16, (os.cpu_count() or 8)))
     t0 = time.time()
     real = args.circuit == "real" and not args.lookups
-    gc, proofs = make_workload(args.degree_bits, args.distinct, args.witnesses, rank + 1, threads, args.lookups, real)
+    arities = tuple(int(a) for a in args.arities.split(",") if a)
+    gc, proofs = make_workload(args.degree_bits, args.distinct, args.witnesses, rank + 1, threads, args.lookups, real, args.ext, arities)
     log(f"[rank {rank}] generated {len(proofs)} distinct proofs in {time.time() - t0:.1f}s")
-    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey, args.ext)
     info = vk.info
     packed = vk.pack_many(proofs)
     B = args.batch
@@ -553,10 +559,11 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "u64 (Goldilocks mod-p integer)", "data": "synthetic",
             "config": {"workload": f"{'C3' if args.lookups else 'C2'}: {B} std-config Plonky2 proofs per GPU per step (degree_bits {info.degree_bits}, "
                                    f"{'real circuit of the recursion gate set, ' if real else 'degenerate circuit, '}"
-                                   f"28 FRI queries, arity 16, deg-2 ext{', lookups: 256 + 65536-entry tables' if args.lookups > 1 else (', lookups' if args.lookups else '')}), "
+                                   f"28 FRI queries, {'arity bits ' + str(list(info.step_arity_bits)) if arities else 'arity 16'}, deg-2 ext{', lookups: 256 + 65536-entry tables' if args.lookups > 1 else (', lookups' if args.lookups else '')}), "
                                    f"{len(proofs)} distinct repeated, 1/16 corrupted, device-resident"
                                    f"{' in 64-proof tiles' if lay_tiled else ' proof-major'}",
                        "global_batch": B * world, "degree_bits": info.degree_bits, "parallelism": f"proof-sharded x{world}",
+                       **({"ext": args.ext} if args.ext else {}),
                        "inflight": nv},
             "serial": {"value": round(total / dt_serial, 1), "ms_per_step": round(dt_serial / args.steps * 1e3, 4),
                        "note": "one batch at a time, host-synchronised per step; kernel_ms and roofline come from this pass"},
@@ -566,7 +573,7 @@ def main():
                          "note": "integer-VALU bound (Poseidon); HBM fraction reported as the metric asks"},
             "valu": {"perms_per_proof": ppp, "perm_rate_G": round(value / world * ppp / 1e9, 3),
                      "issue": valu_roofline(kavg, dt / args.steps * 1e3, B)
-                     if (real and info.degree_bits == 12 and not args.lookups) else None},   # the PMC pass's own workload only
+                     if (real and info.degree_bits == 12 and not args.lookups and not args.ext and not arities) else None},   # the PMC pass's own workload only
             "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
             "verified_all": ok,
         }
