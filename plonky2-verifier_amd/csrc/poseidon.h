@@ -169,6 +169,94 @@ static __constant__ RcSplit c_rc_split = make_rc_split();
 static __constant__ ZhConst c_zh = make_zh();
 #endif
 
+// ---------------------------------------------------------------- merged partial rounds
+// A partial round changes only word 0 before its MDS, so D consecutive partial rounds need
+// only D scalars through the S-box.  With s' = the block's input state after the first S-box
+// (y1 in word 0) and y_k the S-box output of round k of the block, the state after the block is
+//   out = G_D s' + sum_{m=2..D} H_D[:,m] y_m + d_D,   G_1 = M, G_k = M[:,1:] G_{k-1}[1:,:],
+//   H_k[:,k] = M[:,0], H_k[:,m] = M[:,1:] H_{k-1}[1:,m] (m < k),
+//   d_1 = rc[r+1], d_k = M[:,1:] d_{k-1}[1:] + rc[r+k]  (mod p),
+// and the S-box input of round k+1 is row 0 of the same expression at depth k.  Because the
+// MDS entries are < 2^6 and non-negative, every entry of G_k and H_k stays non-negative and
+// small (row sums < 2^(8k)): up to D = 4 a row is still a dot product over the 32-bit halves
+// of 64-bit words that cannot overflow (row sums < 2^31.8, so al, ah < 2^64), with one
+// reduction per row.  The 22 partial rounds then cost 6 blocks of (D S-boxes + D-1 chain rows
+// + 12 output rows) instead of 22 full MDS layers: about 4 000 VALU instead of 7 900.
+// Same function as Hash/Poseidon.hs:48-60 (partialRound, mdsLayer) applied 22 times.
+struct PBlock {
+  uint32_t cf[14][16];      // rows: chain k = 2, 3 at [k - 2], output row i at [2 + i]; G coefs [0..11], H (m = 2..D-1) at [12 + m - 2]
+  uint64_t dlo[16], dhi[16];  // halves of d: chain k = 1..D-1 at [k - 1], output row i at [4 + i]
+};
+#ifndef P2V_PMERGE
+#define P2V_PMERGE 4   // partial rounds per block: 4 (blocks 4,4,4,4,4,2), 3 (3 x 7 + 1), 2 (2 x 11), 0 (one MDS per round)
+#endif
+#if P2V_PMERGE == 4
+static constexpr int PM_NB = 6;
+static constexpr int PM_SCHED[PM_NB] = {4, 4, 4, 4, 4, 2};
+#elif P2V_PMERGE == 3
+static constexpr int PM_NB = 8;
+static constexpr int PM_SCHED[PM_NB] = {3, 3, 3, 3, 3, 3, 3, 1};
+#else
+static constexpr int PM_NB = 11;
+static constexpr int PM_SCHED[PM_NB] = {2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2};
+#endif
+struct PMTab { PBlock b[PM_NB]; };
+__host__ __device__ constexpr uint64_t cx_addp(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a + b) % gl::P); }
+__host__ __device__ constexpr uint64_t cx_mulp(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) % gl::P); }
+__host__ __device__ constexpr int pm_rounds() { int n = 0; for (int b = 0; b < PM_NB; b++) n += PM_SCHED[b]; return n; }
+static_assert(pm_rounds() == 22, "the merge schedule must cover the 22 partial rounds");
+__host__ __device__ constexpr PMTab make_pm() {
+  PMTab T{};
+  constexpr uint64_t rc[360] = P2V_ALL_ROUND_CONSTANTS_INIT;
+  uint64_t G[5][12][12] = {}, H[5][5][12] = {};   // H[k][m][i]
+  for (int i = 0; i < 12; i++)
+    for (int j = 0; j < 12; j++) G[1][i][j] = mds_coeff(i, j);
+  for (int k = 2; k <= 4; k++) {
+    for (int i = 0; i < 12; i++) {
+      for (int j = 0; j < 12; j++) {
+        uint64_t a = 0;
+        for (int l = 1; l < 12; l++) a += mds_coeff(i, l) * G[k - 1][l][j];
+        G[k][i][j] = a;
+      }
+      for (int m = 2; m < k; m++) {
+        uint64_t a = 0;
+        for (int l = 1; l < 12; l++) a += mds_coeff(i, l) * H[k - 1][m][l];
+        H[k][m][i] = a;
+      }
+      H[k][k][i] = mds_coeff(i, 0);
+    }
+  }
+  int r = 4;
+  for (int b = 0; b < PM_NB; b++) {
+    const int D = PM_SCHED[b];
+    uint64_t d[5][12] = {};
+    for (int i = 0; i < 12; i++) d[1][i] = rc[12 * (r + 1) + i] % gl::P;
+    for (int k = 2; k <= D; k++)
+      for (int i = 0; i < 12; i++) {
+        uint64_t a = rc[12 * (r + k) + i] % gl::P;
+        for (int l = 1; l < 12; l++) a = cx_addp(a, cx_mulp(mds_coeff(i, l), d[k - 1][l]));
+        d[k][i] = a;
+      }
+    PBlock& B = T.b[b];
+    for (int k = 1; k < D; k++) { B.dlo[k - 1] = d[k][0] & 0xFFFFFFFFull; B.dhi[k - 1] = d[k][0] >> 32; }
+    for (int k = 2; k < D; k++) {
+      for (int j = 0; j < 12; j++) B.cf[k - 2][j] = (uint32_t)G[k][0][j];
+      for (int m = 2; m < k; m++) B.cf[k - 2][12 + m - 2] = (uint32_t)H[k][m][0];
+    }
+    for (int i = 0; i < 12; i++) {
+      for (int j = 0; j < 12; j++) B.cf[2 + i][j] = (uint32_t)G[D][i][j];
+      for (int m = 2; m < D; m++) B.cf[2 + i][12 + m - 2] = (uint32_t)H[D][m][i];
+      B.dlo[4 + i] = d[D][i] & 0xFFFFFFFFull;
+      B.dhi[4 + i] = d[D][i] >> 32;
+    }
+    r += D;
+  }
+  return T;
+}
+#if defined(__HIPCC__)
+static __constant__ PMTab c_pm = make_pm();
+#endif
+
 #if defined(__HIP_DEVICE_COMPILE__)
 namespace dv {
 // acc + C a as one v_mad_u64_u32 with the matrix entry C as an inline constant.  The carry-out
@@ -306,6 +394,120 @@ __device__ __forceinline__ void round_pp(uint64_t* s, uint64_t* t, int r, bool z
   if (g & 4) mds_rows<8, 12>(s, t, kl, kh);
 #endif
 }
+
+// ---- merged partial rounds (see PBlock): coefficients are wave-uniform table entries (SGPR
+// operands; gfx950 VOP3 takes no literal, and one SGPR per instruction, so the row's first
+// MAD -- the one that takes the SGPR-pair constant as its addend -- is the newest y with its
+// inline MDS entry)
+__device__ __forceinline__ uint64_t madv(uint32_t a, uint32_t c, uint64_t acc) {
+  uint64_t d;
+  asm("v_mad_u64_u32 %0, s[94:95], %1, %2, %3" : "=v"(d) : "v"(a), "s"(c), "v"(acc) : "s94", "s95");
+  return d;
+}
+// al + 2^32 ah for row sums < 2^24 (D <= 3): as reduce_rows, the carry fix-up without a branch
+__device__ __forceinline__ uint64_t reduce_t(uint64_t al, uint64_t ah) {
+  using namespace gl::ax;
+  uint64_t c0, c1, c2;
+  const uint64_t t = madm1_co((uint32_t)(ah >> 32), al, c0);   // < 2^57: no carry
+  const uint32_t rh = add_co((uint32_t)(t >> 32), (uint32_t)ah, c1);
+  return madm1_co(mask_1(c1), ((uint64_t)rh << 32) | (uint32_t)t, c2);
+}
+// al + 2^32 ah for al, ah < 2^64 (D = 4): lo = al + ah_lo 2^32 (carry c), hi = ah_hi + c < 2^32,
+// then lo + hi (2^32 - 1) with one wrap fix-up (the wrapped sum is < hi 2^32, no second wrap).  5 VALU.
+__device__ __forceinline__ uint64_t reduce_w(uint64_t al, uint64_t ah) {
+  using namespace gl::ax;
+  uint64_t c0, c1, c2;
+  const uint32_t lh = add_co((uint32_t)(al >> 32), (uint32_t)ah, c0);
+  const uint32_t hi = addc0((uint32_t)(ah >> 32), c0);
+  const uint64_t r = madm1_co(hi, ((uint64_t)lh << 32) | (uint32_t)al, c1);
+  return madm1_co(mask_1(c1), r, c2);
+}
+// one row: (newest y) * CI + sum_j cf[j] s'_j + sum_m cf[12 + m] y_{m+2} + (dl, dh)
+template <uint32_t CI, int NH>
+__device__ __forceinline__ void prow(const uint64_t* s, const uint64_t* yh, uint64_t yn, const uint32_t* cf,
+                                     uint64_t dl, uint64_t dh, uint64_t& al, uint64_t& ah) {
+  al = madk_s<CI>((uint32_t)yn, dl);
+  ah = madk_s<CI>((uint32_t)(yn >> 32), dh);
+#pragma unroll
+  for (int j = 0; j < 12; j++) {
+    al = madv((uint32_t)s[j], cf[j], al);
+    ah = madv((uint32_t)(s[j] >> 32), cf[j], ah);
+  }
+#pragma unroll
+  for (int m = 0; m < NH; m++) {
+    al = madv((uint32_t)yh[m], cf[12 + m], al);
+    ah = madv((uint32_t)(yh[m] >> 32), cf[12 + m], ah);
+  }
+}
+template <int D, int I>
+__device__ __forceinline__ void pblock_rows(const uint64_t* s, const uint64_t* y, uint64_t* t, const PBlock& B) {
+  if constexpr (I < 12) {
+    uint64_t al, ah;
+    prow<mds_coeff(I, 0), D - 2>(s, y + 2, y[D], B.cf[2 + I], B.dlo[4 + I], B.dhi[4 + I], al, ah);
+    t[I] = D == 4 ? reduce_w(al, ah) : reduce_t(al, ah);
+    pblock_rows<D, I + 1>(s, y, t, B);
+  }
+}
+#if P2V_MDS_BRANCH == 2
+// D = 2 output row before its (rare: ~2^-15) carry fix-up, as row_unfixed
+template <int I>
+__device__ __forceinline__ void prow2_unfixed(const uint64_t* s, uint64_t y2, const PBlock& B, uint64_t& r, uint64_t& c) {
+  using namespace gl::ax;
+  uint64_t al, ah, c0;
+  prow<mds_coeff(I, 0), 0>(s, nullptr, y2, B.cf[2 + I], B.dlo[4 + I], B.dhi[4 + I], al, ah);
+  const uint64_t tt = madm1_co((uint32_t)(ah >> 32), al, c0);   // < 2^49: no carry
+  const uint32_t rh = add_co((uint32_t)(tt >> 32), (uint32_t)ah, c);
+  r = ((uint64_t)rh << 32) | (uint32_t)tt;
+}
+template <int I>
+__device__ __forceinline__ void pblock2_group(const uint64_t* s, uint64_t y2, uint64_t* t, const PBlock& B) {
+  using namespace gl::ax;
+  uint64_t r0, r1, r2, r3, c0, c1, c2, c3, d;
+  prow2_unfixed<I>(s, y2, B, r0, c0);
+  prow2_unfixed<I + 1>(s, y2, B, r1, c1);
+  prow2_unfixed<I + 2>(s, y2, B, r2, c2);
+  prow2_unfixed<I + 3>(s, y2, B, r3, c3);
+  if (__builtin_expect((c0 | c1 | c2 | c3) != 0, 0)) {
+    r0 = madm1_co(mask_1(c0), r0, d);
+    r1 = madm1_co(mask_1(c1), r1, d);
+    r2 = madm1_co(mask_1(c2), r2, d);
+    r3 = madm1_co(mask_1(c3), r3, d);
+  }
+  t[I] = r0; t[I + 1] = r1; t[I + 2] = r2; t[I + 3] = r3;
+}
+#endif
+// D partial rounds: s = the state entering the block's first round (its constants included),
+// t = the state entering the round after the block.  s is clobbered.
+template <int D>
+__device__ __forceinline__ void pblock(uint64_t* s, uint64_t* t, const PBlock& B) {
+  uint64_t y[D + 1];
+  s[0] = sbox_dev(s[0]);   // y1, word 0 of s'
+  {   // chain row 1 (row 0 of M s' + d1): inline MDS entries
+    uint64_t al = madk_s<mds_coeff(0, 0)>((uint32_t)s[0], B.dlo[0]);
+    uint64_t ah = madk_s<mds_coeff(0, 0)>((uint32_t)(s[0] >> 32), B.dhi[0]);
+    mds_acc<0, 1>(s, al, ah);
+    y[2] = sbox_dev(reduce_rows(al, ah));
+  }
+  if constexpr (D >= 3) {   // chain row 2: row sums < 2^16, the branch form of the fix-up
+    uint64_t al, ah;
+    prow<mds_coeff(0, 0), 0>(s, nullptr, y[2], B.cf[0], B.dlo[1], B.dhi[1], al, ah);
+    y[3] = sbox_dev(reduce_rows(al, ah));
+  }
+  if constexpr (D >= 4) {   // chain row 3: row sums < 2^24
+    uint64_t al, ah;
+    prow<mds_coeff(0, 0), 1>(s, y + 2, y[3], B.cf[1], B.dlo[2], B.dhi[2], al, ah);
+    y[4] = sbox_dev(reduce_t(al, ah));
+  }
+#if P2V_MDS_BRANCH == 2
+  if constexpr (D == 2) {
+    pblock2_group<0>(s, y[2], t, B);
+    pblock2_group<4>(s, y[2], t, B);
+    pblock2_group<8>(s, y[2], t, B);
+    return;
+  }
+#endif
+  pblock_rows<D, 0>(s, y, t, B);
+}
 }  // namespace dv
 
 // Device permutation, one per lane.  zh: state words 8..11 are 0 on entry (2-to-1 compression,
@@ -327,11 +529,16 @@ __device__ __forceinline__ void permute_dev(uint64_t s[12], bool zh = false, int
   asm("" : "+s"(fl));
   zh = fl & 8;
   gm = fl & 7;
+  // round 0's constants through an opaque pointer: a caller's loop must not hoist their loads
+  // (with the merged partial rounds' table loads the SGPRs are full, and the hoisted values
+  // would be spilled to VGPR lanes and read back with a VALU op each)
+  const uint64_t* rc0 = c_round_constants;
+  asm volatile("" : "+s"(rc0));
 #pragma unroll
-  for (int i = 0; i < 8; i++) s[i] = add_nc(s[i], c_round_constants[i]);
+  for (int i = 0; i < 8; i++) s[i] = add_nc(s[i], rc0[i]);
   if (!zh) {
 #pragma unroll
-    for (int i = 8; i < 12; i++) s[i] = add_nc(s[i], c_round_constants[i]);
+    for (int i = 8; i < 12; i++) s[i] = add_nc(s[i], rc0[i]);
   }
 #pragma unroll 1
   for (int k = 0; k < 4; k++) {   // full-round pairs (0,1) (2,3) (26,27) (28,29)
@@ -339,11 +546,39 @@ __device__ __forceinline__ void permute_dev(uint64_t s[12], bool zh = false, int
     dv::round_pp<true>(s, t, r, zh && k == 0, 7);
     dv::round_pp<true>(t, s, r + 1, false, k == 3 ? gm : 7);
     if (k == 1) {
+#if P2V_PMERGE == 4
+      // blocks of 4, 4, 4, 4, 4, 2 merged partial rounds; each loop trip reads its own table
+      // copies, so the coefficient loads stay inside the loop (no SGPR spills)
+#pragma unroll 1
+      for (int b = 0; b < 4; b += 2) {
+        dv::pblock<4>(s, t, c_pm.b[b]);
+        dv::pblock<4>(t, s, c_pm.b[b + 1]);
+      }
+      dv::pblock<4>(s, t, c_pm.b[4]);
+      dv::pblock<2>(t, s, c_pm.b[5]);
+#elif P2V_PMERGE == 3
+#pragma unroll 1
+      for (int b = 0; b < 6; b += 2) {
+        dv::pblock<3>(s, t, c_pm.b[b]);
+        dv::pblock<3>(t, s, c_pm.b[b + 1]);
+      }
+      dv::pblock<3>(s, t, c_pm.b[6]);
+      dv::round_pp<false>(t, s, 25, false, 7);
+#elif P2V_PMERGE == 2
+#pragma unroll 1
+      for (int b = 0; b < 10; b += 2) {
+        dv::pblock<2>(s, t, c_pm.b[b]);
+        dv::pblock<2>(t, s, c_pm.b[b + 1]);
+      }
+      dv::round_pp<false>(s, t, 24, false, 7);
+      dv::round_pp<false>(t, s, 25, false, 7);
+#else
 #pragma unroll 1
       for (int q = 4; q < 26; q += 2) {   // partial-round pairs
         dv::round_pp<false>(s, t, q, false, 7);
         dv::round_pp<false>(t, s, q + 1, false, 7);
       }
+#endif
     }
   }
 #pragma unroll
