@@ -80,6 +80,7 @@ struct p2v_verifier {
   hipStream_t side = nullptr;
   float last_ms[kNumKernels] = {0};
   bool timed = false;
+  bool fri_first = false;           // side stream order: k_fri before the vanishing kernels (env P2V_FRI_FIRST=1)
   int transcript_mode = 0;          // 0 auto, 1 row, 2 quad, 3 lane (env P2V_TRANSCRIPT)
   int quad_min_batch = 2048;        // auto: quad form from this batch size on
   bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
@@ -280,6 +281,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (const char* sp = getenv("P2V_SIDE_PRIO")) v->side_prio = sp[0] == '1';
   if (const char* ds = getenv("P2V_DEBUG_SYNC")) v->debug_sync = ds[0] == '1';
   if (const char* f1 = getenv("P2V_PHASE1")) v->split_phase1 = !strcmp(f1, "split");
+  if (const char* ff = getenv("P2V_FRI_FIRST")) v->fri_first = ff[0] == '1';
   if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : !strcmp(tm, "lane") ? 3 : 0;
   DevCircuit& d = v->dc;
   memset(&d, 0, sizeof d);
@@ -543,6 +545,14 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   }
   // phase 2: Merkle paths on the main stream; FRI queries and the vanishing kernel (few,
   // long-latency waves) on the side stream, concurrently
+  // k_fri first: it needs only phase 1 and is the shorter chain, so the vanishing kernels
+  // (longest waves, most registers) are what remains when k_merkle's waves retire
+  if (v->fri_first) {
+    T0(3, sd);
+    k_fri<<<(d.Q * NPB + 3) / 4, 256, 0, sd>>>(d);
+    DBG("k_fri", sd);
+    T1(3, sd);
+  }
   T0(7, sd);
   if (d.n_lut_pieces > 0) k_lut<<<(d.r * d.n_lut_pieces * NPB + 3) / 4, 256, 0, sd>>>(d);
   DBG("k_lut", sd);
@@ -560,10 +570,12 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   k_vanish_final<<<(d.B + 255) / 256, 256, 0, sd>>>(d);
   DBG("k_vanish_final", sd);
   T1(6, sd);
-  T0(3, sd);
-  k_fri<<<(d.Q * NPB + 3) / 4, 256, 0, sd>>>(d);
-  DBG("k_fri", sd);
-  T1(3, sd);
+  if (!v->fri_first) {
+    T0(3, sd);
+    k_fri<<<(d.Q * NPB + 3) / 4, 256, 0, sd>>>(d);
+    DBG("k_fri", sd);
+    T1(3, sd);
+  }
   if (sd != st) HCK(hipEventRecord(v->dep_side, sd));
   T0(2, st);
   k_merkle<<<(leaf_units + 3) / 4, 256, 0, st>>>(d);

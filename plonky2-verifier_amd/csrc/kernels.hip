@@ -589,6 +589,8 @@ extern "C" __global__ void __launch_bounds__(256) k_fri(DevCircuit c) {
 // precedence inside a round (Plonk/Verifier.hs:62, Plonk/FRI.hs:370-407, 105-117, 306-313).
 extern "C" __global__ void __launch_bounds__(256) k_status(DevCircuit c, int8_t* __restrict__ results, uint64_t* __restrict__ trace,
                                                            int64_t trace_words) {
+  // a few short waves that gate the workspace's next batch: ahead of co-resident phase-1 waves
+  __builtin_amdgcn_s_setprio(3);
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= c.n) return;
   const bool eqs_ok = c.van[p] != 0;
