@@ -81,7 +81,7 @@ struct p2v_verifier {
   float last_ms[kNumKernels] = {0};
   bool timed = false;
   bool fri_first = false;           // side stream order: k_fri before the vanishing kernels (env P2V_FRI_FIRST=1)
-  int transcript_mode = 0;          // 0 auto, 1 row, 2 quad, 3 lane (env P2V_TRANSCRIPT)
+  int transcript_mode = 0;          // 0 auto, 1 row, 2 quad (env P2V_TRANSCRIPT)
   int quad_min_batch = 2048;        // auto: quad form from this batch size on
   bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
   int side_prio = 0;                // env P2V_SIDE_PRIO=1: side stream at the device's highest priority (measured: no effect)
@@ -282,7 +282,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (const char* ds = getenv("P2V_DEBUG_SYNC")) v->debug_sync = ds[0] == '1';
   if (const char* f1 = getenv("P2V_PHASE1")) v->split_phase1 = !strcmp(f1, "split");
   if (const char* ff = getenv("P2V_FRI_FIRST")) v->fri_first = ff[0] == '1';
-  if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : !strcmp(tm, "lane") ? 3 : 0;
+  if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : 0;
   DevCircuit& d = v->dc;
   memset(&d, 0, sizeof d);
   d.r = C.r; d.Q = C.num_queries; d.S = (int)C.arities.size(); d.T = 4 + d.S;
@@ -517,7 +517,6 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   int tl = d.B >= v->quad_min_batch ? 4 : 16;
   if (v->transcript_mode == 1) tl = 16;
   else if (v->transcript_mode == 2) tl = 4;
-  else if (v->transcript_mode == 3) tl = 1;
   const int nt_blocks = (tl * d.B + 255) / 256;
   const int leaf_units = d.Q * d.T * NPB;
   if (!v->split_phase1 || sd == st) {

@@ -272,105 +272,11 @@ __device__ __forceinline__ void transcript_quad(const DevCircuit& c, int p, int 
   }
 }
 
-// Lane form of the same transcript: one lane per proof, the state in 24 VGPRs and the
-// throughput permutation (p2::permute_dev, merged partial rounds).  The longest chain of the
-// three forms (~11 k instructions per permutation on one lane) but the fewest issue slots in
-// total (64 proofs per wave, no idle S-box lanes in partial rounds): the form for batches
-// large enough that two in flight hide the chain.  Rate-part words are addressed with
-// wave-uniform indices through unrolled selects (no dynamically indexed registers).
-__device__ __forceinline__ uint64_t lane_word(const uint64_t s[12], int i) {
-  uint64_t v = s[0];
-#pragma unroll
-  for (int j = 1; j < 8; j++) v = i == j ? s[j] : v;
-  return v;
-}
-__device__ __forceinline__ void lane_set(uint64_t s[12], int i, uint64_t v) {
-#pragma unroll
-  for (int j = 0; j < 8; j++) s[j] = i == j ? v : s[j];
-}
-__device__ __forceinline__ void transcript_lane(const DevCircuit& c, int p) {
-  // public inputs hash, Hash/Sponge.hs:26-31 (sponge [] = zero digest)
-  uint64_t s[12];
-#pragma unroll
-  for (int j = 0; j < 12; j++) s[j] = 0;
-  for (int i = 0; i < c.num_pis; i += 8) {
-    const int k = c.num_pis - i;
-#pragma unroll
-    for (int j = 0; j < 8; j++) if (j < k) s[j] = ld(c, c.pis + i + j, p);
-    p2::permute_dev(s);
-  }
-#pragma unroll
-  for (int w = 0; w < 4; w++) chal(c, CH_PI(c) + w, p) = s[w];   // read back where it is absorbed
-#pragma unroll
-  for (int j = 0; j < 12; j++) s[j] = 0;
-  int nbuf = 0, outpos = -1;
-  bool absorbing = true;
-  const uint64_t qmask = (1ULL << c.lde_bits) - 1;
-  uint64_t fa0 = 0, fa1 = 0;   // FRI alpha, kept in registers for the reduced openings below
-  for (int o = 0; o < c.ntops; o++) {
-    const int type = c.tops[3 * o], a = c.tops[3 * o + 1], n = c.tops[3 * o + 2];
-    if (type == TOP_COPY) {   // mkLookupDeltaList (betas ++ gammas ++ ...), Challenge/Verifier.hs:36-40,82-86
-      for (int k = 0; k < n; k++) chal(c, a + k, p) = chal(c, a - 3 * c.r + k, p);
-      continue;
-    }
-    if (type == TOP_ZERO) {
-      for (int k = 0; k < n; k++) chal(c, a + k, p) = 0;
-      continue;
-    }
-    // one permutation call site for the whole op (an inlined permutation is ~40 KB of code):
-    // each trip takes either a whole rate block of absorbed words (buffer empty or full, 8
-    // words left: overwrite words 0..7 at compile-time positions) or a single word
-    const bool ab = type <= TOP_ABSORB_DIGEST;
-    if (ab && !absorbing) { absorbing = true; nbuf = 0; }
-    for (int k = 0; k < n;) {
-      const bool blk = type == TOP_ABSORB_SOA && n - k >= 8 && (nbuf == 0 || nbuf == 8);
-      const bool need = ab ? nbuf == 8 : (absorbing || outpos < 0);
-      if (need) p2::permute_dev(s);   // duplex / re-permute, Challenge/Pure.hs:38-69
-      if (ab) {
-        if (blk) {
-#pragma unroll
-          for (int j = 0; j < 8; j++) s[j] = ld(c, (int64_t)a + k + j, p);   // overwrite mode: the rate part is replaced
-          nbuf = 8;
-          k += 8;
-        } else {
-          uint64_t v0;
-          if (type == TOP_ABSORB_SOA) v0 = ld(c, (int64_t)a + k, p);
-          else if (type == TOP_ABSORB_PIH) v0 = chal(c, CH_PI(c) + (k & 3), p);
-          else v0 = c.digest[k & 3];
-          if (need) nbuf = 0;
-          lane_set(s, nbuf, v0);
-          nbuf++;
-          k++;
-        }
-      } else {   // squeeze: output order state[7], state[6], ... (reverse of take 8)
-        if (need) { absorbing = false; outpos = 7; }
-        uint64_t w = lane_word(s, outpos);
-        outpos--;
-        if (type == TOP_SQUEEZE_IDX) w &= qmask;
-        if (a + k == CH_FRI_ALPHA(c)) fa0 = w;
-        if (a + k == CH_FRI_ALPHA(c) + 1) fa1 = w;
-        chal(c, a + k, p) = w;
-        k++;
-      }
-    }
-  }
-  // precomputeReducedOpenings, Plonk/FRI.hs:128-134: Y = sum alpha^i y_i by Horner
-  const E alpha{fa0, fa1};
-#pragma unroll 1
-  for (int b = 0; b < 2; b++) {
-    const int64_t n = b == 0 ? c.n_this : c.n_next, off = b == 0 ? c.o_const : c.o_zs_next;
-    E h = gl::e0();
-    for (int64_t i = n - 1; i >= 0; i--) h = gl::eadd(gl::emul(h, alpha), lde(c, off + 2 * i, p));
-    chal(c, (b == 0 ? CH_Y0(c) : CH_Y1(c)), p) = h.a;
-    chal(c, (b == 0 ? CH_Y0(c) : CH_Y1(c)) + 1, p) = h.b;
-  }
-}
-
 // ------------------------------------------------------------------------ phase 1
-// blocks [0, nt_blocks): transcripts, `tl` lanes per proof (16: row form, 4: quad form, 1: lane form) at
+// blocks [0, nt_blocks): transcripts, `tl` lanes per proof (16: row form, 4: quad form) at
 // raised wave priority so co-resident leaf waves do not stretch the serial chain; the
 // rest: leaf hashing, 4 units per block.  Transcript blocks come first so they start first.
-extern "C" __global__ void __launch_bounds__(256) k_phase1(DevCircuit c, int nt_blocks, int tl) {
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_phase1(DevCircuit c, int nt_blocks, int tl) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if ((int)blockIdx.x < nt_blocks) {
     __builtin_amdgcn_s_setprio(3);
@@ -379,10 +285,8 @@ extern "C" __global__ void __launch_bounds__(256) k_phase1(DevCircuit c, int nt_
       rp::Row R;
       rp::init(R, threadIdx.x);
       if ((g >> 4) < c.B) transcript_row(c, g >> 4, R);
-    } else if (tl == 4) {
-      if ((g >> 2) < c.B) transcript_quad(c, g >> 2, g & 3);
     } else {
-      if (g < c.B) transcript_lane(c, g);
+      if ((g >> 2) < c.B) transcript_quad(c, g >> 2, g & 3);
     }
     return;
   }
@@ -402,10 +306,8 @@ extern "C" __global__ void __launch_bounds__(256) k_transcript(DevCircuit c, int
     rp::Row R;
     rp::init(R, threadIdx.x);
     if ((g >> 4) < c.B) transcript_row(c, g >> 4, R);
-  } else if (tl == 4) {
-    if ((g >> 2) < c.B) transcript_quad(c, g >> 2, g & 3);
   } else {
-    if (g < c.B) transcript_lane(c, g);
+    if ((g >> 2) < c.B) transcript_quad(c, g >> 2, g & 3);
   }
 }
 extern "C" __global__ void __launch_bounds__(256) k_leaf(DevCircuit c) {

@@ -205,49 +205,61 @@ __host__ __device__ constexpr uint64_t cx_addp(uint64_t a, uint64_t b) { return 
 __host__ __device__ constexpr uint64_t cx_mulp(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) % gl::P); }
 __host__ __device__ constexpr int pm_rounds() { int n = 0; for (int b = 0; b < PM_NB; b++) n += PM_SCHED[b]; return n; }
 static_assert(pm_rounds() == 22, "the merge schedule must cover the 22 partial rounds");
-__host__ __device__ constexpr PMTab make_pm() {
-  PMTab T{};
-  constexpr uint64_t rc[360] = P2V_ALL_ROUND_CONSTANTS_INIT;
-  uint64_t G[5][12][12] = {}, H[5][5][12] = {};   // H[k][m][i]
+// G_k, H_k of the block algebra above (k = 1..4), exact non-negative integers
+struct PMAlg { uint64_t G[5][12][12], H[5][5][12]; };   // H[k][m][i]
+__host__ __device__ constexpr PMAlg pm_alg() {
+  PMAlg A{};
   for (int i = 0; i < 12; i++)
-    for (int j = 0; j < 12; j++) G[1][i][j] = mds_coeff(i, j);
+    for (int j = 0; j < 12; j++) A.G[1][i][j] = mds_coeff(i, j);
   for (int k = 2; k <= 4; k++) {
     for (int i = 0; i < 12; i++) {
       for (int j = 0; j < 12; j++) {
         uint64_t a = 0;
-        for (int l = 1; l < 12; l++) a += mds_coeff(i, l) * G[k - 1][l][j];
-        G[k][i][j] = a;
+        for (int l = 1; l < 12; l++) a += mds_coeff(i, l) * A.G[k - 1][l][j];
+        A.G[k][i][j] = a;
       }
       for (int m = 2; m < k; m++) {
         uint64_t a = 0;
-        for (int l = 1; l < 12; l++) a += mds_coeff(i, l) * H[k - 1][m][l];
-        H[k][m][i] = a;
+        for (int l = 1; l < 12; l++) a += mds_coeff(i, l) * A.H[k - 1][m][l];
+        A.H[k][m][i] = a;
       }
-      H[k][k][i] = mds_coeff(i, 0);
+      A.H[k][k][i] = mds_coeff(i, 0);
     }
   }
+  return A;
+}
+// d_1..d_D (mod p) of the block of D partial rounds starting at round r
+struct PMD { uint64_t d[5][12]; };
+__host__ __device__ constexpr PMD pm_d(int r, int D) {
+  PMD R{};
+  constexpr uint64_t rc[360] = P2V_ALL_ROUND_CONSTANTS_INIT;
+  for (int i = 0; i < 12; i++) R.d[1][i] = rc[12 * (r + 1) + i] % gl::P;
+  for (int k = 2; k <= D; k++)
+    for (int i = 0; i < 12; i++) {
+      uint64_t a = rc[12 * (r + k) + i] % gl::P;
+      for (int l = 1; l < 12; l++) a = cx_addp(a, cx_mulp(mds_coeff(i, l), R.d[k - 1][l]));
+      R.d[k][i] = a;
+    }
+  return R;
+}
+__host__ __device__ constexpr PMTab make_pm() {
+  PMTab T{};
+  const PMAlg A = pm_alg();
   int r = 4;
   for (int b = 0; b < PM_NB; b++) {
     const int D = PM_SCHED[b];
-    uint64_t d[5][12] = {};
-    for (int i = 0; i < 12; i++) d[1][i] = rc[12 * (r + 1) + i] % gl::P;
-    for (int k = 2; k <= D; k++)
-      for (int i = 0; i < 12; i++) {
-        uint64_t a = rc[12 * (r + k) + i] % gl::P;
-        for (int l = 1; l < 12; l++) a = cx_addp(a, cx_mulp(mds_coeff(i, l), d[k - 1][l]));
-        d[k][i] = a;
-      }
+    const PMD dd = pm_d(r, D);
     PBlock& B = T.b[b];
-    for (int k = 1; k < D; k++) { B.dlo[k - 1] = d[k][0] & 0xFFFFFFFFull; B.dhi[k - 1] = d[k][0] >> 32; }
+    for (int k = 1; k < D; k++) { B.dlo[k - 1] = dd.d[k][0] & 0xFFFFFFFFull; B.dhi[k - 1] = dd.d[k][0] >> 32; }
     for (int k = 2; k < D; k++) {
-      for (int j = 0; j < 12; j++) B.cf[k - 2][j] = (uint32_t)G[k][0][j];
-      for (int m = 2; m < k; m++) B.cf[k - 2][12 + m - 2] = (uint32_t)H[k][m][0];
+      for (int j = 0; j < 12; j++) B.cf[k - 2][j] = (uint32_t)A.G[k][0][j];
+      for (int m = 2; m < k; m++) B.cf[k - 2][12 + m - 2] = (uint32_t)A.H[k][m][0];
     }
     for (int i = 0; i < 12; i++) {
-      for (int j = 0; j < 12; j++) B.cf[2 + i][j] = (uint32_t)G[D][i][j];
-      for (int m = 2; m < D; m++) B.cf[2 + i][12 + m - 2] = (uint32_t)H[D][m][i];
-      B.dlo[4 + i] = d[D][i] & 0xFFFFFFFFull;
-      B.dhi[4 + i] = d[D][i] >> 32;
+      for (int j = 0; j < 12; j++) B.cf[2 + i][j] = (uint32_t)A.G[D][i][j];
+      for (int m = 2; m < D; m++) B.cf[2 + i][12 + m - 2] = (uint32_t)A.H[D][m][i];
+      B.dlo[4 + i] = dd.d[D][i] & 0xFFFFFFFFull;
+      B.dhi[4 + i] = dd.d[D][i] >> 32;
     }
     r += D;
   }

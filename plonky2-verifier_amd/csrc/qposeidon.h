@@ -82,6 +82,123 @@ __device__ __forceinline__ void mds_acc(const uint64_t x[3], int t, const uint64
   qrow<2, 0>(X, al[2], ah[2], c00);
 }
 
+// ---- merged partial rounds in the quad layout (p2::PBlock algebra).  The merged matrices are
+// not circulant, so the rotation trick above does not make their coefficients uniform:
+//  * chain rows (row 0 of each level) are evaluated in lane 0's frame, where rotation d, slot k
+//    holds word 3d + k, with the wave-uniform p2::c_pm coefficients, and broadcast from lane 0;
+//  * output rows 3t + m use per-lane coefficients from QBlock (cf[t][m][3d + k] = G_D[3t + m]
+//    [3((t + d) & 3) + k], the y terms after them), loaded at the start of the block.
+struct QBlock {
+  uint32_t cf[4][3][16];   // [t][m]: 12 word coefficients in rotation order, then H_D[m'][3t + m] for m' = 2..D
+  uint64_t d[4][3];        // d_D[3t + m]
+};
+struct QMTab { QBlock b[p2::PM_NB]; };
+__host__ __device__ constexpr QMTab make_qm() {
+  QMTab T{};
+  const p2::PMAlg A = p2::pm_alg();
+  int r = 4;
+  for (int b = 0; b < p2::PM_NB; b++) {
+    const int D = p2::PM_SCHED[b];
+    const p2::PMD dd = p2::pm_d(r, D);
+    for (int t = 0; t < 4; t++)
+      for (int m = 0; m < 3; m++) {
+        const int i = 3 * t + m;
+        for (int d = 0; d < 4; d++)
+          for (int k = 0; k < 3; k++) T.b[b].cf[t][m][3 * d + k] = (uint32_t)A.G[D][i][3 * ((t + d) & 3) + k];
+        for (int mm = 2; mm <= D; mm++) T.b[b].cf[t][m][12 + mm - 2] = (uint32_t)A.H[D][mm][i];
+        T.b[b].d[t][m] = dd.d[D][i];
+      }
+    r += D;
+  }
+  return T;
+}
+#if P2V_PMERGE
+static __constant__ QMTab c_qm = make_qm();
+#endif
+#if P2V_PMERGE && defined(__HIP_DEVICE_COMPILE__)
+#define P2V_QMERGE 1
+
+// acc + a c, c a per-lane VGPR coefficient
+__device__ __forceinline__ uint64_t madl(uint32_t a, uint32_t c, uint64_t acc) {
+  return (uint64_t)a * c + acc;
+}
+// lane-0 frame dot product of the rotated state with 12 uniform coefficients (template: inline
+// MDS row 0 for level 1, else a c_pm chain row)
+template <int K>
+__device__ __forceinline__ void chain_part(const uint64_t (&X)[4][3], const p2::PBlock& B, uint64_t& al, uint64_t& ah) {
+  al = B.dlo[K - 1];
+  ah = B.dhi[K - 1];
+#pragma unroll
+  for (int q = 0; q < 12; q++) {
+    const uint64_t w = X[q / 3][q % 3];
+    uint32_t c;
+    if constexpr (K == 1) c = p2::mds_coeff(0, q);
+    else c = B.cf[K - 2][q];
+    al += (uint64_t)(uint32_t)w * c;
+    ah += (w >> 32) * c;
+  }
+}
+template <int D>
+__device__ __forceinline__ void qblock(uint64_t x[3], int t, const p2::PBlock& B, const QBlock& Q) {
+  // y1 = sbox(word 0) from lane 0; s' = the state with y1 in word 0
+  uint64_t y[D + 1];
+  y[1] = bcast64(p2::sbox_lat(x[0]), 0);
+  x[0] = t == 0 ? y[1] : x[0];
+  uint64_t X[4][3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) { X[0][k] = x[k]; X[1][k] = rot64<1>(x[k]); X[2][k] = rot64<2>(x[k]); X[3][k] = rot64<3>(x[k]); }
+  // the chain: z_k = part_k + sum_{m=2..k} H_k[m][0] y_m, y_{k+1} = sbox(z_k); part_k, the
+  // s'-part of chain row k, is evaluated in lane 0's frame and broadcast (it does not depend on
+  // the S-box chain, so the scheduler can overlap it with the previous S-box)
+  uint64_t pl[D], ph[D];
+  chain_part<1>(X, B, pl[1], ph[1]);
+  pl[1] = bcast64(pl[1], 0); ph[1] = bcast64(ph[1], 0);
+  if constexpr (D >= 3) { chain_part<2>(X, B, pl[2], ph[2]); pl[2] = bcast64(pl[2], 0); ph[2] = bcast64(ph[2], 0); }
+  y[2] = p2::sbox_lat(p2::mds_reduce(pl[1], ph[1]));
+  if constexpr (D >= 4) { chain_part<3>(X, B, pl[3], ph[3]); pl[3] = bcast64(pl[3], 0); ph[3] = bcast64(ph[3], 0); }
+  if constexpr (D >= 3) {
+    constexpr uint32_t c = p2::mds_coeff(0, 0);
+    y[3] = p2::sbox_lat(p2::mds_reduce(pl[2] + (uint64_t)(uint32_t)y[2] * c, ph[2] + (y[2] >> 32) * c));
+  }
+  // per-lane output-row coefficients, one row at a time (row m + 1's loads overlap row m), the
+  // first row's before the last S-box: 17 VGPRs in flight instead of 51
+  uint32_t cf[3][12 + D - 1];
+  uint64_t dq[3];
+  const auto load_row = [&](int m) {
+#pragma unroll
+    for (int j = 0; j < 12 + D - 1; j++) cf[m][j] = Q.cf[t][m][j];
+    dq[m] = Q.d[t][m];
+  };
+  if constexpr (D >= 4) {
+    constexpr uint32_t c = p2::mds_coeff(0, 0);
+    const uint32_t h2 = B.cf[1][12];
+    const uint64_t al = pl[3] + (uint64_t)(uint32_t)y[2] * h2 + (uint64_t)(uint32_t)y[3] * c;
+    const uint64_t ah = ph[3] + (y[2] >> 32) * h2 + (y[3] >> 32) * c;
+    load_row(0);
+    y[4] = p2::sbox_lat(p2::mds_reduce(al, ah));
+  } else {
+    load_row(0);
+  }
+  // output rows 3t + m
+#pragma unroll
+  for (int m = 0; m < 3; m++) {
+    if (m < 2) load_row(m + 1);
+    uint64_t al = dq[m] & 0xFFFFFFFFull, ah = dq[m] >> 32;
+#pragma unroll
+    for (int q = 0; q < 12; q++) {
+      al = madl((uint32_t)X[q / 3][q % 3], cf[m][q], al);
+      ah = madl((uint32_t)(X[q / 3][q % 3] >> 32), cf[m][q], ah);
+    }
+#pragma unroll
+    for (int mm = 2; mm <= D; mm++) {
+      al = madl((uint32_t)y[mm], cf[m][12 + mm - 2], al);
+      ah = madl((uint32_t)(y[mm] >> 32), cf[m][12 + mm - 2], ah);
+    }
+    x[m] = D == 4 ? p2::dv::reduce_w(al, ah) : p2::dv::reduce_t(al, ah);
+  }
+}
+#endif
+
 // the quad's permutation; x = this lane's three words (inputs < 2^64, outputs canonical).
 // Partial rounds take the S-box off the critical path: the MDS runs on the state with word 0
 // zeroed while lane 0's S-box chain is in flight, then sbox(word 0), broadcast from lane 0,
@@ -97,6 +214,52 @@ __device__ __forceinline__ void permute(uint64_t x[3], int t) {
                             t == 0 ? 20u : t == 1 ? 39u : t == 2 ? 28u : 41u,
                             t == 0 ? 34u : t == 1 ? 13u : t == 2 ? 2u : 15u};
   uint64_t kl[3], kh[3], nkl[3], nkh[3];
+#if P2V_QMERGE
+  // full rounds 0..3, the merged partial-round blocks, full rounds 26..29
+  lane_rc(1, t, nkl, nkh);
+#pragma unroll 1
+  for (int r = 0; r < 8; r++) {
+    if (r == 4) {
+#if P2V_PMERGE == 4
+#pragma unroll 1
+      for (int b = 0; b < 5; b++) qblock<4>(x, t, p2::c_pm.b[b], c_qm.b[b]);
+      qblock<2>(x, t, p2::c_pm.b[5], c_qm.b[5]);
+#elif P2V_PMERGE == 3
+#pragma unroll 1
+      for (int b = 0; b < 7; b++) qblock<3>(x, t, p2::c_pm.b[b], c_qm.b[b]);
+#else
+#pragma unroll 1
+      for (int b = 0; b < 11; b++) qblock<2>(x, t, p2::c_pm.b[b], c_qm.b[b]);
+#endif
+      lane_rc(27, t, nkl, nkh);
+    }
+#if P2V_PMERGE == 3
+    if (r == 4) {   // the schedule's single plain partial round (25)
+      lane_rc(26, t, kl, kh);
+      const uint64_t w0 = x[0];
+      x[0] = t == 0 ? 0 : w0;
+      uint64_t al[3], ah[3];
+      mds_acc(x, t, kl, kh, al, ah);
+      const uint64_t sb = bcast64(p2::sbox_lat(w0), 0);
+#pragma unroll
+      for (int m = 0; m < 3; m++) { al[m] += (uint64_t)(uint32_t)sb * col0[m]; ah[m] += (sb >> 32) * col0[m]; }
+#pragma unroll
+      for (int m = 0; m < 3; m++) x[m] = p2::mds_reduce(al[m], ah[m]);
+    }
+#endif
+    const int rr = r < 4 ? r : r + 22;   // 0..3, 26..29
+#pragma unroll
+    for (int k = 0; k < 3; k++) { kl[k] = nkl[k]; kh[k] = nkh[k]; }
+    lane_rc(rr + 2 <= 30 ? rr + 2 : 30, t, nkl, nkh);   // row 30 of the split table is zero
+    uint64_t al[3], ah[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) x[k] = p2::sbox_lat(x[k]);
+    mds_acc(x, t, kl, kh, al, ah);
+#pragma unroll
+    for (int m = 0; m < 3; m++) x[m] = p2::mds_reduce(al[m], ah[m]);
+  }
+  (void)col0;
+#else
   lane_rc(1, t, nkl, nkh);
 #pragma unroll 1
   for (int r = 0; r < 30; r++) {
@@ -122,6 +285,7 @@ __device__ __forceinline__ void permute(uint64_t x[3], int t) {
 #pragma unroll
     for (int m = 0; m < 3; m++) x[m] = p2::mds_reduce(al[m], ah[m]);
   }
+#endif
 #pragma unroll
   for (int k = 0; k < 3; k++) x[k] = gl::canon(x[k]);
 }
