@@ -347,7 +347,7 @@ C5_PROOFS = 1 << 20       # BASELINE.json configs[4]: 1M proofs over the node's 
 C5_CHUNK = 131072         # per launch: C5's per-GPU share on 8 GPUs
 
 
-def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, backend, dist, streams, tiled, steps=1):
+def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, backend, dist, streams, tiled, steps=1, stagger=0):
     """BASELINE.json configs[4] (C5): 1 048 576 std proofs sharded over the ranks (contiguous
     shards, p2v.shard_bounds), each rank verifying its shard in launches of up to 131 072 proofs
     (the per-GPU share at 8 GPUs) on two workspaces in flight.  The shard is device-resident:
@@ -364,6 +364,9 @@ def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, backend, dis
         big = d_proofs.repeat(reps, 1)[:rows].contiguous()
     exp = d_expect.repeat(reps)[:rows]
     bvs = [p2v.BatchVerifier(vk, local, rows) for _ in range(2)]
+    if stagger:
+        bvs[0].chain(bvs[1])
+        bvs[1].chain(bvs[0])
     res = [torch.empty(rows, dtype=torch.int8, device=dev) for _ in range(2)]
     chunks = [min(rows, n - k) for k in range(0, n, rows)]
 
@@ -411,6 +414,8 @@ def main():
                          "degenerate: gate filters 0 (required with --lookups: the real prover has no lookup argument)")
     ap.add_argument("--degree-bits", type=int, default=12)
     ap.add_argument("--inflight", type=int, default=2, help="batches in flight per GPU (workspaces/streams)")
+    ap.add_argument("--stagger", type=int, default=0, choices=(0, 1),
+                    help="1: chain the in-flight workspaces (p2v_verifier_chain) so their phase 1 alternate")
     ap.add_argument("--layout", choices=("tiled", "proof-major"), default="tiled",
                     help="device-resident batch layout: 64-proof tiles (P2V_FLAG_INPUT_TILED, coalesced loads) or proof-major rows")
     ap.add_argument("--ext", type=int, default=0, help="P2V_EXT_* flags of the workload circuit (1 MinSize arities, 2 hiding, 4 hash_or_noop)")
@@ -484,6 +489,9 @@ def main():
     nv = max(1, args.inflight)
     d_res = [torch.empty(B, dtype=torch.int8, device=dev) for _ in range(nv)]
     bvs = [p2v.BatchVerifier(vk, local, B) for _ in range(nv)]
+    if args.stagger and nv > 1:   # workspace j's phase 1 follows workspace j-1's (cyclically)
+        for j in range(nv):
+            bvs[j].chain(bvs[j - 1])
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nv - 1)]
 
     def timed(k, pipelined):
@@ -531,7 +539,8 @@ def main():
     kavg = {k: float(np.mean(v)) for k, v in ktimes.items()}
     c5 = None
     if not args.quick and not args.no_c5:
-        c5 = c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, args.dist_backend, dist, streams, lay_tiled)
+        c5 = c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, args.dist_backend, dist, streams, lay_tiled,
+                    stagger=args.stagger)
     if rank == 0:
         kb = kernel_bytes_model(info, info.trace_words)
         # dominant kernel: the longest launch on the main stream (k_transcript / k_vanish / k_fri /
@@ -564,7 +573,7 @@ def main():
                                    f"{' in 64-proof tiles' if lay_tiled else ' proof-major'}",
                        "global_batch": B * world, "degree_bits": info.degree_bits, "parallelism": f"proof-sharded x{world}",
                        **({"ext": args.ext} if args.ext else {}),
-                       "inflight": nv},
+                       "inflight": nv, "stagger": bool(args.stagger and nv > 1)},
             "serial": {"value": round(total / dt_serial, 1), "ms_per_step": round(dt_serial / args.steps * 1e3, 4),
                        "note": "one batch at a time, host-synchronised per step; kernel_ms and roofline come from this pass"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",

@@ -218,6 +218,16 @@ void p2v_verifier_free(p2v_verifier* v);
 int  p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n,
                       int8_t* results, uint64_t* trace, void* stream, uint32_t flags);
 
+/* Stagger two or more workspaces that run back-to-back batches on their own streams: after
+ * p2v_verifier_chain(v, prev), every later run of v starts its phase 1 (transcript + leaf
+ * hashing) only once the phase 1 most recently enqueued on prev has finished (a device-side
+ * event wait; the host never blocks).  Chaining two verifiers to each other alternates their
+ * phase 1 with the other batch's Merkle / FRI / vanishing work instead of running both batches'
+ * phases in lockstep.  prev = NULL removes the link.  Results are unaffected; v and prev must be
+ * on the same device, and prev must outlive the link (unlink, or free v first).  Not part of
+ * the reference (a batching schedule). */
+int  p2v_verifier_chain(p2v_verifier* v, p2v_verifier* prev);
+
 /* Verify n proofs given as ProofWithPublicInputs JSON texts (Types.hs:245-279) in host memory:
  * proof i is blob[offsets[i] .. offsets[i+1]) (n + 1 offsets; pinned memory makes the copy
  * fastest).  The texts are copied to the device and packed there against a template taken

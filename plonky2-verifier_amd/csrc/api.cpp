@@ -77,6 +77,9 @@ struct p2v_verifier {
   DevBuf t_cs, t_kis, t_gkind, t_gpar, t_ggrp, t_gwoff, t_w, t_gs, t_ge, t_lin, t_lout, t_loff, t_llen, t_tw, t_ops, t_vit, t_rin, t_rout, t_roff, t_rch, t_pbase;
   hipEvent_t ev[2 * kNumKernels];   // start/end per kernel
   hipEvent_t dep_p1 = nullptr, dep_side = nullptr, dep_tr = nullptr;
+  hipEvent_t p1_done = nullptr;      // recorded on the caller's stream after phase 1 (p2v_verifier_chain)
+  bool p1_recorded = false;
+  p2v_verifier* chain_prev = nullptr;
   hipStream_t side = nullptr;
   float last_ms[kNumKernels] = {0};
   bool timed = false;
@@ -262,9 +265,17 @@ void p2v_verifier_free(p2v_verifier* v) {
   if (v->dep_p1) (void)hipEventDestroy(v->dep_p1);
   if (v->dep_side) (void)hipEventDestroy(v->dep_side);
   if (v->dep_tr) (void)hipEventDestroy(v->dep_tr);
+  if (v->p1_done) (void)hipEventDestroy(v->p1_done);
   if (v->side) (void)hipStreamDestroy(v->side);
   if (v->h_res) (void)hipHostFree(v->h_res);
   delete v;
+}
+
+int p2v_verifier_chain(p2v_verifier* v, p2v_verifier* prev) {
+  if (!v) return fail(P2V_E_ARG, "null verifier");
+  if (prev && prev->device != v->device) return fail(P2V_E_ARG, "p2v_verifier_chain: verifiers on different devices");
+  v->chain_prev = prev;
+  return P2V_OK;
 }
 
 int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v_verifier** out) {
@@ -431,6 +442,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_p1, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_side, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_tr, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&v->p1_done, hipEventDisableTiming);
   // the side stream carries few, long-latency waves (vanishing items, FRI queries); a
   // high-priority queue for it was measured (P2V_SIDE_PRIO=1) and changed nothing
   if (e == hipSuccess) {
@@ -519,6 +531,8 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   else if (v->transcript_mode == 2) tl = 4;
   const int nt_blocks = (tl * d.B + 255) / 256;
   const int leaf_units = d.Q * d.T * NPB;
+  // staggered workspaces (p2v_verifier_chain): phase 1 after the linked workspace's latest one
+  if (v->chain_prev && v->chain_prev->p1_recorded) HCK(hipStreamWaitEvent(st, v->chain_prev->p1_done, 0));
   if (!v->split_phase1 || sd == st) {
     T0(1, st);
     k_phase1<<<nt_blocks + (leaf_units + 3) / 4, 256, 0, st>>>(d, nt_blocks, tl);
@@ -542,6 +556,8 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     T1(8, st);
     HCK(hipStreamWaitEvent(st, v->dep_tr, 0));   // k_merkle reads the query indices
   }
+  HCK(hipEventRecord(v->p1_done, st));   // k_merkle's inputs are complete on st here in both forms
+  v->p1_recorded = true;
   // phase 2: Merkle paths on the main stream; FRI queries and the vanishing kernel (few,
   // long-latency waves) on the side stream, concurrently
   // k_fri first: it needs only phase 1 and is the shorter chain, so the vanishing kernels

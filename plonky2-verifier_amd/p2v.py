@@ -128,6 +128,7 @@ def lib() -> ctypes.CDLL:
     L.p2v_verifier_free.argtypes = [vp]
     L.p2v_verifier_free.restype = None
     L.p2v_verifier_run.argtypes = [vp, u64p, sz, i8p, u64p, vp, ctypes.c_uint32]
+    L.p2v_verifier_chain.argtypes = [vp, vp]
     L.p2v_verifier_run_json.argtypes = [vp, vp, vp, sz, i8p, vp, vp, vp]
     L.p2v_verifier_pack_json.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp]
     L.p2v_verifier_run_bytes.argtypes = [vp, vp, vp, sz, i8p, vp, vp, vp]
@@ -391,6 +392,13 @@ class BatchVerifier:
         k = lib().p2v_verifier_last_timings(self._h, buf, 16)
         names = lib().p2v_kernel_names().decode().split(",")
         return {names[i]: float(buf[i]) for i in range(k) if buf[i] > 0}   # 0: kernel not launched in this build
+
+    def chain(self, prev: Optional["BatchVerifier"]) -> None:
+        """p2v_verifier_chain: later runs of this workspace start phase 1 after `prev`'s latest
+        phase 1 (staggered workspaces; results unaffected).  prev=None unlinks.  Keeps a
+        reference to prev so it outlives the link."""
+        _check(lib().p2v_verifier_chain(self._h, prev._h if prev is not None else None))
+        self._chain_prev = prev
 
     def __del__(self):
         try:

@@ -226,6 +226,36 @@ def test_gpu_tiled_input_matches_proof_major(p2v, nb, mode, lk):
     assert np.array_equal(dres.cpu().numpy(), r0)
 
 
+def test_gpu_chained_workspaces(p2v):
+    """p2v_verifier_chain: three workspaces chained cyclically on three streams, 9 batches in
+    flight without host syncs (each batch a different rotation of a pool with valid and
+    corrupted proofs): every batch's statuses equal the unchained verifier's; unlinking works."""
+    import torch
+    gc = gen_circuit(6, 4, 0, 1, 28, 16, 0, 1)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    pool = [gc.proof(1, 1), gc.proof(2, 2), gc.proof(1, 3, flags=1), gc.proof(1, 4, flags=4)]
+    packed = vk.pack_many(pool)
+    B = 200
+    batches = [np.ascontiguousarray(packed[(np.arange(B) + k) % len(pool)]) for k in range(9)]
+    want = [p2v.BatchVerifier(vk, 0, B).run(b) for b in batches]
+    bvs = [p2v.BatchVerifier(vk, 0, B) for _ in range(3)]
+    for j in range(3):
+        bvs[j].chain(bvs[j - 1])
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    d_in = [torch.from_numpy(b.view(np.int64)).cuda() for b in batches]
+    d_res = [torch.empty(B, dtype=torch.int8, device="cuda") for _ in batches]
+    torch.cuda.synchronize()
+    for k in range(9):   # workspace k % 3 is reused every third batch: stream order keeps them apart
+        bvs[k % 3].run_device(d_in[k].data_ptr(), B, d_res[k].data_ptr(), stream=streams[k % 3].cuda_stream, sync=False)
+    torch.cuda.synchronize()
+    for k in range(9):
+        assert np.array_equal(d_res[k].cpu().numpy(), want[k]), k
+    assert set(want[0].tolist()) == {1, -3, 0}
+    for bv in bvs:
+        bv.chain(None)
+    assert np.array_equal(bvs[0].run(batches[1]), want[1])
+
+
 def _number_paths(d, path=()):
     """Every number leaf of a JSON value, as a key path."""
     if isinstance(d, dict):
