@@ -50,6 +50,14 @@ __device__ __forceinline__ void step8(uint32_t* x, uint64_t* xx, uint32_t k, uin
 #define CMP64(i) "v_cmp_gt_u64_e64 s[96:97], %" S(i) ", %10\n"
 #define MADK(i) "v_mad_u64_u32 %" S(i) ", s[96:97], %11, 7, %" S(i) "\n"
 #define NOP(i) "s_nop 0\n"
+// VOP2 encodings of the carry-chain ops (carry in / out through VCC) and a VOP3 / VOP2 mix
+#define ADDCO32(i) "v_add_co_u32_e32 %" S(i) ", vcc, %8, %" S(i) "\n"
+#define ADDC32(i) "v_addc_co_u32_e32 %" S(i) ", vcc, %8, %" S(i) ", vcc\n"
+#define SUBB32(i) "v_subb_co_u32_e32 %" S(i) ", vcc, %8, %" S(i) ", vcc\n"
+#define CND32(i) "v_cndmask_b32_e32 %" S(i) ", %8, %" S(i) ", vcc\n"
+#define MIX(i) ADDCO(i) ADDC32(i)
+#define X16(I) X8(I) X8(I)
+#define AV(str) asm volatile(str : R32 : "v"(k), "s"(kk), "v"(kk), "v"(k2) : "s96", "s97", "vcc")
   if constexpr (OP == 0) A64(X32(MAD));
   if constexpr (OP == 1) A(X32(MULHI));
   if constexpr (OP == 2) A(X32(MULLO));
@@ -67,12 +75,19 @@ __device__ __forceinline__ void step8(uint32_t* x, uint64_t* xx, uint32_t k, uin
   if constexpr (OP == 14) A64(X32(CMP64));
   if constexpr (OP == 15) A64(X32(MADK));
   if constexpr (OP == 16) A(X32(NOP));
+  if constexpr (OP == 17) AV(X32(ADDCO32));
+  if constexpr (OP == 18) AV(X32(ADDC32));
+  if constexpr (OP == 19) AV(X32(SUBB32));
+  if constexpr (OP == 20) AV(X32(CND32));
+  if constexpr (OP == 21) AV(X16(MIX));
 }
 static const char* kOpNames[] = {
   "v_mad_u64_u32", "v_mul_hi_u32", "v_mul_lo_u32", "v_add_co_u32", "v_sub_co_u32", "v_addc_co_u32",
   "v_cndmask_b32", "v_lshl_add_u64", "v_add_u32", "v_xor_b32", "v_add3_u32", "v_mad_u32_u24", "v_mov_b32",
-  "v_lshlrev_b64", "v_cmp_gt_u64", "v_mad_u64_u32 (const)", "s_nop 0"};
-constexpr int NOPS = 17;
+  "v_lshlrev_b64", "v_cmp_gt_u64", "v_mad_u64_u32 (const)", "s_nop 0",
+  "v_add_co_u32_e32 (VOP2, vcc)", "v_addc_co_u32_e32 (VOP2, vcc)", "v_subb_co_u32_e32 (VOP2, vcc)", "v_cndmask_b32_e32 (VOP2, vcc)",
+  "mix: v_add_co_u32_e64 + v_addc_co_u32_e32"};
+constexpr int NOPS = 22;
 
 struct Clk { unsigned long long t0, t1, r0, r1; };
 
