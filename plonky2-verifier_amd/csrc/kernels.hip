@@ -316,7 +316,15 @@ extern "C" __global__ void __launch_bounds__(256) k_leaf(DevCircuit c) {
 }
 
 // ------------------------------------------------------------------------ Merkle paths
-extern "C" __global__ void __launch_bounds__(256) k_merkle(DevCircuit c) {
+#ifndef P2V_MERKLE_WAVES
+#define P2V_MERKLE_WAVES 6   // amdgpu_waves_per_eu on k_merkle: 77 VGPRs, 6 waves/SIMD, no scratch (serial +4.7 %, pipelined unchanged; 0 = compiler default, 5 waves)
+#endif
+#if P2V_MERKLE_WAVES > 0
+#define P2V_MERKLE_ATTR __attribute__((amdgpu_waves_per_eu(P2V_MERKLE_WAVES)))
+#else
+#define P2V_MERKLE_ATTR
+#endif
+extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCircuit c) {
   const int lane = threadIdx.x & 63;
   const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int NPB = c.B >> 6;
