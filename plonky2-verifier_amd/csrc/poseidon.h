@@ -144,7 +144,8 @@ __host__ __device__ __forceinline__ void partial_round(uint64_t s[12], int r) {
 //    constant (the compiler otherwise turns 2/16 into 64-bit shifts of zero-extended register
 //    pairs and pays a v_mov per pair);
 //  * rounds alternate between two register sets (s -> t -> s), so no copies are needed at
-//    loop edges; full rounds run as 4 pairs, partial rounds as 11 pairs.
+//    loop edges; full rounds run as 4 pairs, the 22 partial rounds as merged blocks (PBlock,
+//    P2V_PMERGE; 11 pairs of single rounds with P2V_PMERGE=0).
 struct RcSplit { uint64_t lo[31 * 12], hi[31 * 12]; };   // round 30 = 0 (after the last MDS)
 __host__ __device__ constexpr RcSplit make_rc_split() {
   RcSplit t{};
@@ -532,7 +533,8 @@ __device__ __forceinline__ void pblock(uint64_t* s, uint64_t* t, const PBlock& B
 //  * every MDS multiply-add is an explicit v_mad_u64_u32 with the matrix entry as an inline
 //    constant;
 //  * rounds alternate between two register sets (s -> t -> s), so no copies are needed at
-//    loop edges; full rounds run as 4 pairs, partial rounds as 11 pairs.
+//    loop edges; full rounds run as 4 pairs, the 22 partial rounds as merged blocks (PBlock,
+//    P2V_PMERGE; 11 pairs of single rounds with P2V_PMERGE=0).
 __device__ __forceinline__ void permute_dev(uint64_t s[12], bool zh = false, int gm = 7) {
   uint64_t t[12];
   // keep zh / gm run-time uniform values (uniform branches); as compile-time constants the

@@ -7,7 +7,8 @@
 // DPP quad_perm rotations (lane t reads lane (t+d) & 3), which makes the circulant
 // coefficient of every term wave-uniform: M(3t+m, 3((t+d)&3)+k) = circ[(3d + k - m) mod 12]
 // (+8 on the diagonal entry (0,0), Hash/Constants.hs:21-25).  ~3.6x lower latency per
-// permutation than one lane holding all 12 words.
+// permutation than one lane holding all 12 words.  The 22 partial rounds run as the merged
+// blocks of poseidon.h (PBlock) in this layout (qblock below).
 #pragma once
 #include "gl.h"
 #include "poseidon.h"
