@@ -404,7 +404,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=None,
                     help="GPUs (= ranks). Under torchrun it must equal WORLD_SIZE; without torchrun and N > 1 "
                          "bench.py starts the N ranks itself (torch.distributed.run child process)")
-    ap.add_argument("--steps", type=int, default=100)   # ~0.5 s timed: long enough for an external utilisation sampler
+    ap.add_argument("--steps", type=int, default=300)   # ~1.1 s pipelined + ~1.4 s serial timed: long enough for an external utilisation sampler
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096, help="proofs per GPU per step")
     ap.add_argument("--distinct", type=int, default=64, help="distinct generated proofs per rank (repeated to the batch)")
