@@ -154,3 +154,38 @@ def test_merged_rows_cannot_overflow(D):
     # the D = 2 rows and the chain rows 1, 2 use the rare-carry branch form: t < 2^49
     G2, _ = levels(2)
     assert max(sum(r) for r in G2[2]) + max(M[i][0] for i in range(12)) < 2**17
+
+
+def test_cpp_tables_match_model(tmp_path):
+    """The tables the device code reads (csrc/poseidon.h make_pm, dumped on the host by
+    tools/pm_dump.cpp) equal this model's G, H and d for every block of the default schedule:
+    chain rows k = 2..D-1 at cf[k-2] (G_k row 0, then H_k[m][0] for m < k), output rows at
+    cf[2 + i] (G_D row i, then H_D[m][i] for m < D), d_k[0] at d[k-1] and d_D[i] at d[4 + i]."""
+    import json
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no host C++ compiler")
+    root = os.path.join(os.path.dirname(__file__), "..")
+    exe = str(tmp_path / "pm_dump")
+    subprocess.check_call([gxx, "-std=c++17", "-O1", "-o", exe, os.path.join(root, "tools", "pm_dump.cpp")],
+                          stderr=subprocess.DEVNULL)
+    dump = json.loads(subprocess.check_output([exe]))
+    assert dump["sched"] == SCHEDULES[4]
+    r = 4
+    for D, blk in zip(dump["sched"], dump["blocks"]):
+        G, H = levels(D)
+        d = dconsts(r, D)
+        cf, dd = blk["cf"], blk["d"]
+        for k in range(1, D):
+            assert dd[k - 1] == d[k][0], (r, k)
+        for k in range(2, D):
+            assert cf[k - 2][:12] == G[k][0]
+            assert cf[k - 2][12:12 + k - 2] == [H[k][m][0] for m in range(2, k)]
+        for i in range(12):
+            assert cf[2 + i][:12] == G[D][i], (r, i)
+            assert cf[2 + i][12:12 + D - 2] == [H[D][m][i] for m in range(2, D)]
+            assert dd[4 + i] == d[D][i]
+        r += D
+    assert r == 26
