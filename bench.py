@@ -15,8 +15,9 @@ Workload: synthetic valid proofs from the build's prover (csrc/gen): standard re
 config (degree_bits 12, rate_bits 3, cap_height 4, 28 queries, arity 16, PoW 16, 135 wires /
 80 routed, the 14-gate recursion gate set incl. Poseidon + CosetInterpolation).  By default a
 real circuit (gates on rows, selector polynomials, copy constraints, Z / partial products, a
-genuine quotient: every vanishing term non-zero at zeta; --circuit degenerate for the
-gate-filters-0 circuit, which --lookups uses).  D distinct proofs per rank repeated into distinct
+genuine quotient: every vanishing term non-zero at zeta; with --lookups the lookup tables'
+LookupGate / LookupTableGate blocks and a live lookup argument; --circuit degenerate for the
+gate-filters-0 circuit).  D distinct proofs per rank repeated into distinct
 HBM memory, 1/16 of them corrupted (initial Merkle leaf -> -1, last step sibling -> -2).
 Every timed batch's statuses are checked against the expected vector.
 """
@@ -347,12 +348,26 @@ C5_PROOFS = 1 << 20       # BASELINE.json configs[4]: 1M proofs over the node's 
 C5_CHUNK = 131072         # per launch: C5's per-GPU share on 8 GPUs
 
 
-def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, backend, dist, streams, tiled, steps=1, stagger=0):
+def max_over_ranks(dt, world, cpu_grp):
+    """The step time of the slowest rank: an all-reduce MAX of one float64 over the gloo side
+    group (CPU tensor), so the multi-GPU number depends on no RCCL call."""
+    if world == 1:
+        return dt
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=cpu_grp)
+    return float(t.item())
+
+
+def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, cpu_grp, streams, tiled, steps=1, stagger=0):
     """BASELINE.json configs[4] (C5): 1 048 576 std proofs sharded over the ranks (contiguous
     shards, p2v.shard_bounds), each rank verifying its shard in launches of up to 131 072 proofs
     (the per-GPU share at 8 GPUs) on two workspaces in flight.  The shard is device-resident:
     the C2 batch repeated on the device to 131 072 distinct HBM rows, reused by every launch of
-    the shard.  Statuses of every launch are checked.  Time = max over ranks."""
+    the shard.  Statuses of every launch are checked: the result buffers are cleared before the
+    timed pass and each launch's statuses are compared with the expected vector on its own
+    stream, folded into a per-stream device flag.  Time = max over ranks."""
     import torch
     s, e = p2v.shard_bounds(C5_PROOFS, world, int(os.environ.get("RANK", "0")))
     n = e - s
@@ -367,36 +382,43 @@ def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, backend, dis
     if stagger:
         bvs[0].chain(bvs[1])
         bvs[1].chain(bvs[0])
+    import torch.distributed as dist
     res = [torch.empty(rows, dtype=torch.int8, device=dev) for _ in range(2)]
     chunks = [min(rows, n - k) for k in range(0, n, rows)]
+    sts = [streams[j % len(streams)] for j in range(2)]
+    okf = [torch.ones((), dtype=torch.bool, device=dev) for _ in range(2)]
 
-    def one_pass():
+    def one_pass(check):
         for i, c in enumerate(chunks):
-            bvs[i % 2].run_device(big.data_ptr(), c, res[i % 2].data_ptr(), stream=streams[i % 2 % len(streams)].cuda_stream, sync=False,
-                                  tiled=tiled)
-    one_pass()   # warm-up
+            j = i % 2
+            bvs[j].run_device(big.data_ptr(), c, res[j].data_ptr(), stream=sts[j].cuda_stream, sync=False, tiled=tiled)
+            if check:   # this launch's statuses, on its stream, before the buffer is reused
+                with torch.cuda.stream(sts[j]):
+                    okf[j] &= (res[j][:c] == exp[:c]).all()
+    one_pass(False)   # warm-up
+    torch.cuda.synchronize(dev)
+    for r in res:
+        r.zero_()
     torch.cuda.synchronize(dev)
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=cpu_grp)
     t = time.perf_counter()
     for _ in range(steps):
-        one_pass()
+        one_pass(True)
     torch.cuda.synchronize(dev)
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=cpu_grp)
     dt = time.perf_counter() - t
-    ok = all(bool((res[i % 2][:c] == exp[:c]).all()) for i, c in enumerate(chunks[-2:]))
-    tmax = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    dt = float(tmax.item())
+    ok = bool(okf[0].item()) and bool(okf[1].item())
+    dt = max_over_ranks(dt, world, cpu_grp)
     del big, bvs, res
     torch.cuda.empty_cache()
     return {"proofs": C5_PROOFS * steps, "value": round(C5_PROOFS * steps / dt, 1), "unit": "proofs/s",
             "per_gpu": round(C5_PROOFS * steps / dt / world, 1), "seconds": round(dt, 4), "n_gpus": world,
             "shard_per_gpu": n, "launch_proofs": rows, "verified_all": ok,
             "note": "BASELINE configs[4]: 1M std proofs sharded over the ranks (no data-path collective), "
-                    "launches of <= 131072 device-resident proofs, two in flight per GPU; time = max over ranks"}
+                    "launches of <= 131072 device-resident proofs, two in flight per GPU, every launch's statuses checked on "
+                    "the device; time = max over ranks"}
 
 
 def main():
@@ -410,8 +432,8 @@ def main():
     ap.add_argument("--distinct", type=int, default=64, help="distinct generated proofs per rank (repeated to the batch)")
     ap.add_argument("--witnesses", type=int, default=8)
     ap.add_argument("--circuit", choices=("real", "degenerate"), default="real",
-                    help="real: gates on rows, copy constraints, genuine quotient (C4's recursion gate set); "
-                         "degenerate: gate filters 0 (required with --lookups: the real prover has no lookup argument)")
+                    help="real: gates on rows, copy constraints, genuine quotient (C4's recursion gate set; with --lookups "
+                         "also LookupGate / LookupTableGate blocks with a live lookup argument); degenerate: gate filters 0")
     ap.add_argument("--degree-bits", type=int, default=12)
     ap.add_argument("--inflight", type=int, default=2, help="batches in flight per GPU (workspaces/streams)")
     ap.add_argument("--stagger", type=int, default=0, choices=(0, 1),
@@ -444,6 +466,7 @@ def main():
         log("[bench] launching", args.gpus, "ranks:", " ".join(cmd))
         sys.exit(subprocess.call(cmd))
     world = int(env_world or "1")
+    cpu_grp = None
     if args.gpus is not None and args.gpus != world:
         log(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a mislabelled number")
         sys.exit(2)
@@ -459,6 +482,10 @@ def main():
         os.dup2(2, 1)
         try:
             dist.init_process_group(args.dist_backend if torch.cuda.is_available() else "gloo")
+            # the bench's only cross-rank operations (barriers, the max-over-ranks time) run on a
+            # gloo side group over CPU tensors: the proofs shard with no data-path collective, so
+            # no RCCL call is needed for the number
+            cpu_grp = dist.new_group(backend="gloo")
         finally:
             sys.stdout.flush()
             os.dup2(saved, 1)
@@ -470,7 +497,7 @@ def main():
 
     threads = max(1, min(16, (os.cpu_count() or 8)))
     t0 = time.time()
-    real = args.circuit == "real" and not args.lookups
+    real = args.circuit == "real"
     arities = tuple(int(a) for a in args.arities.split(",") if a)
     gc, proofs = make_workload(args.degree_bits, args.distinct, args.witnesses, rank + 1, threads, args.lookups, real, args.ext, arities)
     log(f"[rank {rank}] generated {len(proofs)} distinct proofs in {time.time() - t0:.1f}s")
@@ -500,7 +527,7 @@ def main():
         work); serial: one workspace, synchronous, per-kernel times recorded."""
         ktimes = {}
         if world > 1:
-            dist.barrier()
+            dist.barrier(group=cpu_grp)
         torch.cuda.synchronize(dev)
         t = time.perf_counter()
         for i in range(k):
@@ -512,12 +539,9 @@ def main():
                     ktimes.setdefault(name, []).append(v)
         torch.cuda.synchronize(dev)
         if world > 1:
-            dist.barrier()
+            dist.barrier(group=cpu_grp)
         dt = time.perf_counter() - t
-        tmax = torch.tensor([dt], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
-        if world > 1:
-            dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        return float(tmax.item()), ktimes
+        return max_over_ranks(dt, world, cpu_grp), ktimes
 
     for i in range(args.warmup):
         bvs[i % nv].run_device(d_proofs.data_ptr(), B, d_res[i % nv].data_ptr(), stream=streams[i % nv].cuda_stream, sync=False,
@@ -539,7 +563,7 @@ def main():
     kavg = {k: float(np.mean(v)) for k, v in ktimes.items()}
     c5 = None
     if not args.quick and not args.no_c5:
-        c5 = c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, args.dist_backend, dist, streams, lay_tiled,
+        c5 = c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, cpu_grp, streams, lay_tiled,
                     stagger=args.stagger)
     if rank == 0:
         kb = kernel_bytes_model(info, info.trace_words)

@@ -236,6 +236,26 @@ struct Circuit {
   std::vector<std::vector<u64>> const_h;              // the same columns on H (natural order)
   int q_bits = 0;                                     // log2 of the quotient coset size
   int max_constraints = 0;
+  // real mode with lookup tables (commentary/Lookups.md "Layout"): one block of rows per table,
+  // in row order [LookupGate rows | LookupTableGate rows | NoopGate row].  The running sums read
+  // the block bottom-up (Plonk/Lookups.hs:112-132: RE and SLDC at x take their "next" at omega x).
+  struct LkBlock { int table, lu0, nlu, lut0, nlut, noop; };
+  std::vector<LkBlock> lblocks;
+  std::vector<int8_t> row_lk;                         // [N]: 0 none, 1 LookupGate, 2 LookupTableGate, 3 the block's Noop
+  std::vector<int> row_block;                         // [N]: the block of a lookup row (-1 none)
+};
+
+// lookup geometry of a circuit (Plonk/Lookups.hs:64-68)
+struct LkGeom {
+  int lu_slots, lut_slots, nsl, lu_deg, lut_deg;
+  explicit LkGeom(const Circuit& C)
+      : lu_slots(C.num_routed / 2), lut_slots(C.num_routed / 3), nsl(C.nlp - 1), lu_deg(C.qdf - 1),
+        lut_deg(C.nlp > 1 ? (C.num_routed / 3 + C.nlp - 2) / (C.nlp - 1) : 1) {}
+  // zip truncation of prevThisPairs with the three chunk lists (:115-116)
+  int npairs() const {
+    const int clu = (lu_slots + lu_deg - 1) / lu_deg, clut = (lut_slots + lut_deg - 1) / lut_deg;
+    return std::min(nsl, std::min(clu, clut));
+  }
 };
 
 std::string coset_gate_string(int bits) {
@@ -330,7 +350,6 @@ int measure_degree(const gg::Gate& g, int nw, int nk, Rng& rg) {
 }
 
 void build_real(Circuit& C) {
-  if (!C.luts.empty()) throw std::runtime_error("gen: real mode has no lookup argument prover");
   const int N = C.N, NW = C.num_wires, NR = C.num_routed, NK = C.num_gate_consts;
   Rng rg(C.circuit_seed * 7919 + 17);
   for (int i = 0; i < 4; i++) C.circuit_digest.e[i] = rg.field();
@@ -361,6 +380,40 @@ void build_real(Circuit& C) {
     std::vector<u64> pts(n); pts[0] = 1; for (int i = 1; i < n; i++) pts[i] = gl::mul(pts[i - 1], gsub);
     for (int i = 0; i < n; i++) { u64 pr = 1; for (int j = 0; j < n; j++) if (j != i) pr = gl::mul(pr, gl::sub(pts[i], pts[j])); cg.weights.push_back(gl::inv(pr)); }
   }
+  // lookup tables: one block per table at the end of the rows, [LU | LUT | Noop] in row order;
+  // a LUT row holds 26 (inp, out, mult) slots, a LU row 40 (inp, out) pairs (Lookups.hs:64-65).
+  // Table entries fill the LUT rows from the bottom up (Lookups.md "Layout"): RE(x) = delta^26
+  // RE(omega x) + row(x) then equals evalFinalRE's Horner over the table at the top LUT row.
+  C.lblocks.clear();
+  C.row_lk.assign(N, 0);
+  C.row_block.assign(N, -1);
+  if (!C.luts.empty()) {
+    const LkGeom lg(C);
+    std::vector<Circuit::LkBlock> bl;
+    int total = 0;
+    for (size_t t = 0; t < C.luts.size(); t++) {
+      Circuit::LkBlock b{};
+      b.table = (int)t;
+      b.nlut = (int)((C.luts[t].size() + lg.lut_slots - 1) / lg.lut_slots);
+      b.nlu = 1 + b.nlut / 32;
+      total += b.nlu + b.nlut + 1;
+      bl.push_back(b);
+    }
+    int row = N - total;
+    if (row < (int)C.G.size()) throw std::runtime_error("gen: the lookup tables do not fit in 2^degree_bits rows");
+    for (auto& b : bl) {
+      b.lu0 = row; b.lut0 = b.lu0 + b.nlu; b.noop = b.lut0 + b.nlut; row = b.noop + 1;
+      for (int i = b.lu0; i < b.lut0; i++) C.row_lk[i] = 1;
+      for (int i = b.lut0; i < b.noop; i++) C.row_lk[i] = 2;
+      C.row_lk[b.noop] = 3;
+      for (int i = b.lu0; i <= b.noop; i++) C.row_block[i] = (int)C.lblocks.size();
+      C.lblocks.push_back(b);
+      const std::string h = keccak_str(100 + b.table);
+      C.G.push_back(mkgate(LOOKUP, lg.lu_slots, b.table, 0, "LookupGate { num_slots: " + std::to_string(lg.lu_slots) + ", lut_hash: " + h + " }"));
+      C.G.push_back(mkgate(LOOKUPTABLE, lg.lut_slots, b.table, 0, "LookupTableGate { num_slots: " + std::to_string(lg.lut_slots) +
+                                                                   ", lut_hash: " + h + ", last_lut_row: " + std::to_string(b.noop - 1) + " }"));
+    }
+  }
   // degrees, sorted ascending (plonky2 orders a circuit's gates by degree), selector groups:
   // one group if max_deg + #gates - 1 <= qdf, else greedy ranges with size + degree <= qdf
   Rng drg(99);
@@ -389,9 +442,27 @@ void build_real(Circuit& C) {
     for (auto& g : C.G) { out.clear(); gg::eval(g, w.data(), NW, k.data(), NK, pih.data(), out); C.max_constraints = std::max(C.max_constraints, (int)out.size()); }
   }
   C.num_gate_constraints = C.max_constraints;
-  // rows: every gate once, then random gates; row constants random where the gate reads them
+  // rows: every gate once, then random gates; row constants random where the gate reads them.
+  // Lookup gates appear only in their tables' blocks (with the blocks' Noop rows).
+  std::vector<int> plain;
+  int noop_idx = -1;
+  for (int k = 0; k < NG; k++) {
+    if (C.G[k].kind == gg::NOOP) noop_idx = k;
+    if (C.G[k].kind != gg::LOOKUP && C.G[k].kind != gg::LOOKUPTABLE) plain.push_back(k);
+  }
   C.row_gate.assign(N, 0);
-  for (int i = 0; i < N; i++) C.row_gate[i] = i < NG ? i : (int)(rg.next() % (u64)NG);
+  for (int i = 0; i < N; i++) {
+    if (C.row_lk[i]) {
+      const auto& b = C.lblocks[C.row_block[i]];
+      int k = noop_idx;
+      for (int m = 0; m < NG && C.row_lk[i] != 3; m++)
+        if (C.G[m].p1 == b.table && C.G[m].kind == (C.row_lk[i] == 1 ? gg::LOOKUP : gg::LOOKUPTABLE)) k = m;
+      if (k < 0) throw std::runtime_error("gen: a lookup block needs a NoopGate");
+      C.row_gate[i] = k;
+    } else {
+      C.row_gate[i] = i < (int)plain.size() ? plain[i] : plain[rg.next() % (u64)plain.size()];
+    }
+  }
   C.row_consts.assign((size_t)N * NK, 0);
   for (int i = 0; i < N; i++) {
     int nc = gg::num_row_constants(C.G[C.row_gate[i]]);
@@ -427,6 +498,20 @@ void build_real(Circuit& C) {
   for (int g = 0; g < C.ngroups; g++) {
     std::vector<u64> v(N);
     for (int i = 0; i < N; i++) { int k = C.row_gate[i]; v[i] = C.sel_idx[k] == g ? (u64)k : 0xFFFFFFFFULL; }
+    cols.push_back(std::move(v));
+  }
+  // lookup selectors (commentary/Lookups.md "Lookup selectors"; Lookups.hs:27-41): TransSre on
+  // the LUT rows, TransLdc on the LU rows, InitSre on each block's Noop row, LastLdc on each
+  // block's first LU row, StartEnd_t on the first LUT row of table t
+  for (int s = 0; s < C.nls; s++) {
+    std::vector<u64> v(N, 0);
+    for (const auto& b : C.lblocks) {
+      if (s == 0) for (int i = b.lut0; i < b.noop; i++) v[i] = 1;
+      if (s == 1) for (int i = b.lu0; i < b.lut0; i++) v[i] = 1;
+      if (s == 2) v[b.noop] = 1;
+      if (s == 3) v[b.lu0] = 1;
+      if (s == 4 + b.table) v[b.lut0] = 1;
+    }
     cols.push_back(std::move(v));
   }
   for (int c = 0; c < NK; c++) { std::vector<u64> v(N); for (int i = 0; i < N; i++) v[i] = C.row_consts[(size_t)i * NK + c]; cols.push_back(std::move(v)); }
@@ -640,6 +725,22 @@ Witness* make_witness_real(const Circuit& C, u64 seed) {
   for (auto& x : W->pis) x = rg.field();
   u64 pih[4] = {0, 0, 0, 0};
   if (!W->pis.empty()) sponge(W->pis.data(), W->pis.size(), pih);
+  // ---- lookups: per block the looked-up table entries (witness-random, the last LU row padded
+  // with the table's first entry as plonky2 pads) and each table slot's multiplicity; padded
+  // table slots (copies of the head entry, Lookups.hs:107) carry multiplicity 0
+  const LkGeom lg(C);
+  std::vector<std::vector<uint32_t>> lk_ent(C.lblocks.size());   // [block][nlu * lu_slots] entry index
+  std::vector<std::vector<u64>> lk_mult(C.lblocks.size());       // [block][nlut * lut_slots]
+  for (size_t b = 0; b < C.lblocks.size(); b++) {
+    const auto& B = C.lblocks[b];
+    const auto& lut = C.luts[B.table];
+    const int nslot = B.nlu * lg.lu_slots;
+    const int nreal = std::max(1, nslot - (int)(rg.next() % (u64)(lg.lu_slots / 2 + 1)));
+    lk_ent[b].assign(nslot, 0);
+    for (int s = 0; s < nreal; s++) lk_ent[b][s] = (uint32_t)(rg.next() % (u64)lut.size());
+    lk_mult[b].assign((size_t)B.nlut * lg.lut_slots, 0);
+    for (uint32_t e : lk_ent[b]) lk_mult[b][e] = gl::add(lk_mult[b][e], 1);
+  }
   // ---- wires: rows in order; a copy constraint presets its (free input) destination
   std::vector<u64> rows((size_t)N * NW);
   std::vector<uint8_t> pre(NW);
@@ -656,6 +757,22 @@ Witness* make_witness_real(const Circuit& C, u64 seed) {
     const gg::Gate& g = C.G[C.row_gate[i]];
     const u64* k = &C.row_consts[(size_t)i * NK];
     gg::fill(g, w, pre.data(), NW, k, pih, wrg);
+    if (C.row_lk[i] == 1 || C.row_lk[i] == 2) {   // the slots of a lookup row (the rest stay random)
+      const int b = C.row_block[i];
+      const auto& B = C.lblocks[b];
+      const auto& lut = C.luts[B.table];
+      if (C.row_lk[i] == 1)
+        for (int s = 0; s < lg.lu_slots; s++) {
+          const auto& e = lut[lk_ent[b][(size_t)(i - B.lu0) * lg.lu_slots + s]];
+          w[2 * s] = e.first; w[2 * s + 1] = e.second;
+        }
+      else
+        for (int s = 0; s < lg.lut_slots; s++) {
+          const size_t slot = (size_t)(B.noop - 1 - i) * lg.lut_slots + s;   // entries fill bottom-up
+          const auto& e = lut[slot < lut.size() ? slot : 0];
+          w[3 * s] = e.first; w[3 * s + 1] = e.second; w[3 * s + 2] = lk_mult[b][slot];
+        }
+    }
     out.clear();
     gg::eval(g, w, NW, k, NK, pih, out);
     for (size_t t = 0; t < out.size(); t++)
@@ -676,12 +793,69 @@ Witness* make_witness_real(const Circuit& C, u64 seed) {
   std::vector<u64> betas(r), gammas(r), alphas(r);
   for (auto& b : betas) b = d.squeeze();
   for (auto& g : gammas) g = d.squeeze();
+  // lookup challenges: betas ++ gammas ++ 2r fresh, in chunks of 4 = (A, B, alpha, delta) per
+  // challenge round (Challenge/Verifier.hs:29-40,82-86)
+  std::vector<u64> deltas;
+  if (C.nlp > 0) {
+    deltas = betas; deltas.insert(deltas.end(), gammas.begin(), gammas.end());
+    for (int i = 0; i < 2 * r; i++) deltas.push_back(d.squeeze());
+  }
   // ---- Z and the partial products per challenge round (Vanishing.hs:97-111)
   const int nch = (NR + C.qdf - 1) / C.qdf;   // chunks; partial products = nch - 1 = npp
   const u64 omega = gl::subgroup_gen(n);
   std::vector<u64> om(N); om[0] = 1; for (int i = 1; i < N; i++) om[i] = gl::mul(om[i - 1], omega);
-  W->zw = r * (1 + C.npp);
+  const int LZ = r * (1 + C.npp);             // first lookup column: [Z | partial products | lookup zs]
+  W->zw = LZ + r * C.nlp;
   std::vector<std::vector<u64>> zcols(W->zw, std::vector<u64>(N));
+  // per round and table: evalFinalRE, Horner in delta over the padded table (Lookups.hs:103-109)
+  std::vector<std::vector<u64>> final_re(C.nlp > 0 ? r : 0);
+  for (int j = 0; j < (int)final_re.size(); j++)
+    for (const auto& lut : C.luts) {
+      const u64 Bc = deltas[4 * j + 1], de = deltas[4 * j + 3];
+      const size_t padded = (lut.size() + lg.lut_slots - 1) / lg.lut_slots * lg.lut_slots;
+      u64 acc = 0;
+      for (size_t s = 0; s < padded; s++) {
+        const auto& e = lut[s < lut.size() ? s : 0];
+        acc = gl::add(gl::mul(de, acc), gl::add(e.first, gl::mul(Bc, e.second)));
+      }
+      final_re[j].push_back(acc);
+    }
+  // ---- lookup polynomials per round: RE (column 0) and the SLDC running sums (1..nsl), built
+  // bottom-up through each block so that every Lookups.hs:94-132 term vanishes on H; rows outside
+  // the blocks (and RE on the LU rows) are unconstrained and random
+  for (int j = 0; j < (int)final_re.size(); j++) {
+    const u64 Ac = deltas[4 * j], Bc = deltas[4 * j + 1], al = deltas[4 * j + 2], de = deltas[4 * j + 3];
+    const int L = LZ + j * C.nlp;
+    for (int c = L; c < L + C.nlp; c++) for (int i = 0; i < N; i++) zcols[c][i] = rg.field();
+    for (const auto& B : C.lblocks) {
+      for (int c = L; c < L + C.nlp; c++) zcols[c][B.noop] = 0;
+      for (int i = B.noop - 1; i >= B.lu0; i--) {
+        const u64* w = &rows[(size_t)i * NW];
+        const bool is_lut = i >= B.lut0;
+        u64 prev = zcols[L + lg.nsl][i + 1];
+        for (int k = 0; k < lg.nsl; k++) {
+          u64 sum = 0;
+          if (k < lg.npairs()) {
+            if (is_lut)
+              for (int s = k * lg.lut_deg; s < std::min((k + 1) * lg.lut_deg, lg.lut_slots); s++)
+                sum = gl::add(sum, gl::mul(w[3 * s + 2], gl::inv(gl::sub(al, gl::add(w[3 * s], gl::mul(Ac, w[3 * s + 1]))))));
+            else
+              for (int s = k * lg.lu_deg; s < std::min((k + 1) * lg.lu_deg, lg.lu_slots); s++)
+                sum = gl::sub(sum, gl::inv(gl::sub(al, gl::add(w[2 * s], gl::mul(Ac, w[2 * s + 1])))));
+          }
+          prev = gl::add(prev, sum);
+          zcols[L + 1 + k][i] = prev;
+        }
+        if (is_lut) {
+          u64 re = zcols[L][i + 1];
+          for (int s = 0; s < lg.lut_slots; s++) re = gl::add(gl::mul(de, re), gl::add(w[3 * s], gl::mul(Bc, w[3 * s + 1])));
+          zcols[L][i] = re;
+        }
+      }
+      if (zcols[L + lg.nsl][B.lu0] != 0) throw std::runtime_error("gen: the lookups' log-derivative sum is not zero");
+      if (zcols[L][B.lut0] != final_re[j][B.table]) throw std::runtime_error("gen: the table's running evaluation is not evalFinalRE");
+    }
+  }
   for (int j = 0; j < r; j++) {
     std::vector<u64> num((size_t)N * nch), den((size_t)N * nch);
     parallel_for(N, [&](size_t i) {
@@ -690,7 +864,7 @@ Witness* make_witness_real(const Circuit& C, u64 seed) {
         for (int t = c * C.qdf; t < NR && t < (c + 1) * C.qdf; t++) {
           const u64 w = rows[i * NW + t];
           pn = gl::mul(pn, gl::add(gl::add(w, gl::mul(betas[j], gl::mul(C.k_is[t], om[i]))), gammas[j]));
-          pd = gl::mul(pd, gl::add(gl::add(w, gl::mul(betas[j], C.const_h[C.ngroups + NK + t][i])), gammas[j]));
+          pd = gl::mul(pd, gl::add(gl::add(w, gl::mul(betas[j], C.const_h[C.ngroups + C.nls + NK + t][i])), gammas[j]));
         }
         num[i * nch + c] = pn; den[i * nch + c] = pd;
       }
@@ -710,6 +884,7 @@ Witness* make_witness_real(const Circuit& C, u64 seed) {
   }
   W->zs_coeffs.resize(W->zw);
   parallel_for(W->zw, [&](size_t c) { W->zs_coeffs[c] = interpolate(zcols[c], n); });
+  W->lzs_coeffs.assign(W->zs_coeffs.begin() + LZ, W->zs_coeffs.end());
   W->zs_lde = oracle_rows(W->zs_coeffs, C.lde_bits);
   tree_of_rows(W->zs_lde, W->zw, C.lde_bits, C.cap_height, W->zs_tree, W->salt[1], C.ext & 4);
   d.absorb_digests(W->zs_tree.cap());
@@ -736,14 +911,56 @@ Witness* make_witness_real(const Circuit& C, u64 seed) {
         u64 pn = 1, pd = 1;
         for (int s = c * C.qdf; s < NR && s < (c + 1) * C.qdf; s++) {
           pn = gl::mul(pn, gl::add(gl::add(wq[s][t], gl::mul(gl::mul(betas[j], C.k_is[s]), x)), gammas[j]));
-          pd = gl::mul(pd, gl::add(gl::add(wq[s][t], gl::mul(betas[j], C.const_q[C.ngroups + NK + s][t])), gammas[j]));
+          pd = gl::mul(pd, gl::add(gl::add(wq[s][t], gl::mul(betas[j], C.const_q[C.ngroups + C.nls + NK + s][t])), gammas[j]));
         }
         terms.push_back(gl::sub(gl::mul(prev, pn), gl::mul(next, pd)));
       }
     }
+    // lookup terms per round (Plonk/Lookups.hs:89-132), in the reference's order
+    for (int j = 0; j < (int)final_re.size(); j++) {
+      const u64 Ac = deltas[4 * j], Bc = deltas[4 * j + 1], al = deltas[4 * j + 2], de = deltas[4 * j + 3];
+      const int L = LZ + j * C.nlp;
+      const size_t tn = (t + shift) % MQ;
+      auto sel = [&](int s) { return C.const_q[C.ngroups + s][t]; };
+      auto W_ = [&](int c) { return wq[c][t]; };
+      terms.push_back(gl::mul(sel(3), zq[L + lg.nsl][t]));   // LastLdc: the final SLDC is 0
+      terms.push_back(gl::mul(sel(2), zq[L + 1][t]));        // InitSre: SUM starts at 0
+      terms.push_back(gl::mul(sel(2), zq[L][t]));            // InitSre: RE starts at 0
+      for (size_t k = 0; k < C.luts.size(); k++) terms.push_back(gl::mul(sel(4 + (int)k), gl::sub(zq[L][t], final_re[j][k])));
+      u64 cur = zq[L][tn];
+      for (int s = 0; s < lg.lut_slots; s++) cur = gl::add(gl::mul(de, cur), gl::add(W_(3 * s), gl::mul(Bc, W_(3 * s + 1))));
+      terms.push_back(gl::mul(sel(0), gl::sub(zq[L][t], cur)));
+      // sum_i prod_{j != i} of a chunk's factors, and the full product
+      auto prods = [&](const std::vector<u64>& f, const std::vector<u64>* mult, u64& full, u64& sum1) {
+        full = 1; sum1 = 0;
+        for (size_t i = 0; i < f.size(); i++) {
+          full = gl::mul(full, f[i]);
+          u64 p = mult ? (*mult)[i] : 1;
+          for (size_t m = 0; m < f.size(); m++) if (m != i) p = gl::mul(p, f[m]);
+          sum1 = gl::add(sum1, p);
+        }
+      };
+      std::vector<u64> f, mu;
+      for (int m = 0; m < lg.npairs(); m++) {
+        const u64 prev = m == 0 ? zq[L + lg.nsl][tn] : zq[L + m][t], thiz = zq[L + 1 + m][t];
+        const u64 dlt = gl::sub(thiz, prev);
+        u64 lu_p, lu_s, lut_p, lut_s;
+        f.clear();
+        for (int s = m * lg.lu_deg; s < std::min((m + 1) * lg.lu_deg, lg.lu_slots); s++) f.push_back(gl::sub(al, gl::add(W_(2 * s), gl::mul(Ac, W_(2 * s + 1)))));
+        prods(f, nullptr, lu_p, lu_s);
+        f.clear(); mu.clear();
+        for (int s = m * lg.lut_deg; s < std::min((m + 1) * lg.lut_deg, lg.lut_slots); s++) {
+          f.push_back(gl::sub(al, gl::add(W_(3 * s), gl::mul(Ac, W_(3 * s + 1)))));
+          mu.push_back(W_(3 * s + 2));
+        }
+        prods(f, &mu, lut_p, lut_s);
+        terms.push_back(gl::mul(sel(0), gl::sub(gl::mul(lut_p, dlt), lut_s)));   // SUM transition
+        terms.push_back(gl::mul(sel(1), gl::add(gl::mul(lu_p, dlt), lu_s)));     // LDC transition
+      }
+    }
     std::vector<u64> wv(NW), kv(NK), cons, vsum(TG, 0);
     for (int c = 0; c < NW; c++) wv[c] = wq[c][t];
-    for (int c = 0; c < NK; c++) kv[c] = C.const_q[C.ngroups + c][t];
+    for (int c = 0; c < NK; c++) kv[c] = C.const_q[C.ngroups + C.nls + c][t];
     for (int k = 0; k < NG; k++) {
       const int g = C.sel_idx[k];
       const u64 S = C.const_q[g][t];
@@ -1049,7 +1266,17 @@ void* p2v_gen_circuit_new3(int degree_bits, int num_pis, int lookups, uint64_t c
     C->real = mode != 0; C->gate_set = mode == 2 ? 1 : 0;
     if (num_queries > 0) C->num_queries = num_queries;
     if (pow_bits >= 0) C->pow_bits = pow_bits;
-    if (lookups) {
+    if (lookups >= 4) {
+      // small tables that fit a 64-row circuit: 4 one table of 40 u6 entries; 5 that table and
+      // a 30-entry table with field-sized outputs; 6 the 2^16-entry range table alone
+      C->nlp = 7;
+      std::vector<std::pair<u64, u64>> a, b, c;
+      for (u64 i = 0; i < 40; i++) a.push_back({i, (i * 37 + 11) & 63});
+      for (u64 i = 0; i < 30; i++) b.push_back({1000 + 3 * i, (i * 0x9E3779B97F4A7C15ULL + 5) % 0xFFFFFFFF00000001ULL});
+      for (u64 i = 0; i < 65536; i++) c.push_back({i, 0});
+      if (lookups == 6) C->luts.push_back(c);
+      else { C->luts.push_back(a); if (lookups == 5) C->luts.push_back(b); }
+    } else if (lookups) {
       C->nlp = 7;
       std::vector<std::pair<u64, u64>> t8, t16;
       for (u64 i = 0; i < 256; i++) t8.push_back({i, (i * i + 7) & 255});

@@ -578,10 +578,12 @@ def shard_bounds(n: int, world: int, rank: int):
 
 
 def verify_sharded(vkey: VerifierCircuitData, packed: np.ndarray, rank: int, world: int, device: int,
-                   group=None, verify_shard=None) -> np.ndarray:
+                   group=None, verify_shard=None, gather_group=None) -> np.ndarray:
     """Each rank verifies its shard of `packed` on its own GPU; the int8 statuses are then
     gathered so every rank holds the full result vector (one all_gather of the padded int8
     shards, the only cross-rank traffic; on the RCCL backend the gather runs on the device).
+    gather_group: a gloo group (dist.new_group(backend="gloo")) to gather over instead, on CPU
+    tensors -- the fallback when the RCCL path is unavailable or unwanted.
     verify_shard(rows, start, end) -> int8 statuses replaces the rank's BatchVerifier (tests
     inject a CPU verifier to run the sharding with gloo and no GPU)."""
     s, e = shard_bounds(packed.shape[0], world, rank)
@@ -594,6 +596,8 @@ def verify_sharded(vkey: VerifierCircuitData, packed: np.ndarray, rank: int, wor
     import torch
     import torch.distributed as dist
     longest = shard_bounds(packed.shape[0], world, 0)[1]   # shard 0 is a longest one
+    if gather_group is not None:
+        group = gather_group
     dev = torch.device("cuda", device) if dist.get_backend(group) == "nccl" else torch.device("cpu")
     mine = torch.zeros(max(1, longest), dtype=torch.int8, device=dev)
     mine[: len(local)] = torch.from_numpy(local).to(dev)

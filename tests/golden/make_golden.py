@@ -37,6 +37,17 @@ CASES = [
     # generating it takes ~80 s, so it is a fixture rather than generated in the GPU tests
     ("n16_valid", 16, 0, 16, 1, 1, 0, None),
     ("n16_step_sibling", 16, 0, 16, 1, 1, 0, "sib"),
+    # real circuits (generator modes 1 / 2: gates on rows, selector polynomials, copy
+    # constraints, Z / partial products, a genuine quotient), with and without a live lookup
+    # argument (LookupGate / LookupTableGate blocks, RE and SLDC columns from the witness)
+    ("real_valid", 6, 0, 16, 1, 1, 0, None, 1),
+    ("real_quotient", 6, 0, 16, 1, 6, 4, None, 1),
+    ("real_lookup_valid_a", 6, 5, 16, 1, 1, 0, None, 1),
+    ("real_lookup_valid_b", 6, 5, 16, 2, 3, 0, None, 1),
+    ("real_lookup_re", 6, 5, 16, 1, 1, 0, "lookup_re", 1),
+    ("real_lookup_sel", 6, 5, 16, 1, 1, 0, "lookup_sel", 1),
+    ("real_lookup_small_valid", 6, 4, 16, 3, 2, 0, None, 2),
+    ("real_lookup_small_wire", 6, 4, 16, 3, 2, 0, "lookup_wire", 2),
 ]
 
 
@@ -50,17 +61,24 @@ def apply(name, d):
         d["proof"]["opening_proof"]["pow_witness"] += 1
     elif name == "wire":
         d["proof"]["openings"]["wires"][11][1] += 1
+    elif name == "lookup_re":       # RE of round 1 at zeta (lookup_zs[nlp]): only lookup terms read it
+        d["proof"]["openings"]["lookup_zs"][7][0] += 1
+    elif name == "lookup_sel":      # the TransLdc lookup selector (constants: gate sels | lookup sels | ...)
+        d["proof"]["openings"]["constants"][d["_ngroups"] + 1][1] += 1
+    elif name == "lookup_wire":     # the output of the first lookup slot (wire 1)
+        d["proof"]["openings"]["wires"][1][0] += 1
 
 
 def main():
     O = oracle()
     index = []
     circuits = {}
-    for (name, nb, lk, pb, ws, ps, flags, mut) in CASES:
-        key = (nb, lk, pb)
-        gc = gen_circuit(nb, 4, lk, 1, 28, pb)
+    for case in CASES:
+        (name, nb, lk, pb, ws, ps, flags, mut), mode = case[:8], (case[8] if len(case) > 8 else 0)
+        key = (nb, lk, pb, mode)
+        gc = gen_circuit(nb, 4, lk, 1, 28, pb, 0, mode)
         if key not in circuits:
-            cname = f"circuit_n{nb}_lk{lk}_pow{pb}"
+            cname = f"circuit_n{nb}_lk{lk}_pow{pb}" + (f"_m{mode}" if mode else "")
             circuits[key] = cname
             with gzip.GzipFile(os.path.join(HERE, cname + "_common.json.gz"), "wb", mtime=0) as f:
                 f.write(gc.common)
@@ -68,7 +86,13 @@ def main():
                 f.write(gc.vkey)
         proof = gc.proof(ws, ps, flags)
         if mut:
-            proof = mutate(proof, lambda d: apply(mut, d))
+            ngroups = len(json.loads(gc.common)["selectors_info"]["groups"])
+
+            def f(d):
+                d["_ngroups"] = ngroups
+                apply(mut, d)
+                del d["_ngroups"]
+            proof = mutate(proof, f)
         with gzip.GzipFile(os.path.join(HERE, name + "_proof.json.gz"), "wb", mtime=0) as f:
             f.write(proof)
         st, tr = O.verify_json(gc.common, gc.vkey, proof, trace=True)

@@ -67,9 +67,10 @@ def test_two_rank_gloo_sharded_verification():
     assert got == expect == [1, 0, 1, -3, 1]
 
 
-def _worker_product(rank, world, port, proofs, common, vkey, out):
+def _worker_product(rank, world, port, proofs, common, vkey, out, side=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    side_grp = dist.new_group(backend="gloo") if side else None
     p2v = p2v_module()
     vk = p2v.VerifierCircuitData.from_json(common, vkey)   # host-only: no GPU needed
     packed = vk.pack_many(proofs)
@@ -80,14 +81,14 @@ def _worker_product(rank, world, port, proofs, common, vkey, out):
         assert rows.shape[0] == e - s and np.array_equal(rows, packed[s:e])
         seen.append((s, e))
         return np.array([O.verify_json(common, vkey, proofs[i]) for i in range(s, e)], dtype=np.int8)
-    got = p2v.verify_sharded(vk, packed, rank, world, 0, verify_shard=shard)
+    got = p2v.verify_sharded(vk, packed, rank, world, 0, verify_shard=shard, gather_group=side_grp)
     out.put((rank, seen, got.tolist()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_product_verify_sharded_gather_gloo(world):
+@pytest.mark.parametrize("world,side", [(2, False), (3, False), (2, True)])
+def test_product_verify_sharded_gather_gloo(world, side):
     """p2v.verify_sharded itself (the per-rank path of bench.py / multi-GPU hosts) on gloo:
     every rank verifies exactly its contiguous shard, and every rank ends with the full status
     vector in batch order (uneven shards: 7 proofs over 2 or 3 ranks)."""
@@ -99,7 +100,7 @@ def test_product_verify_sharded_gather_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker_product, args=(r, world, port, proofs, gc.common, gc.vkey, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker_product, args=(r, world, port, proofs, gc.common, gc.vkey, q, side)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]
@@ -110,3 +111,32 @@ def test_product_verify_sharded_gather_gloo(world):
     for rank, seen, got in res:
         assert seen == [p2v.shard_bounds(len(proofs), world, rank)]
         assert got == expect
+
+
+def _worker_max(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    grp = dist.new_group(backend="gloo")
+    dist.barrier(group=grp)
+    out.put((rank, bench.max_over_ranks(0.5 + rank, world, grp)))
+    dist.destroy_process_group()
+
+
+def test_bench_max_over_ranks_on_gloo_side_group():
+    """bench.py's step time is the slowest rank's, reduced over a gloo side group on CPU
+    tensors (the 8-GPU run needs no RCCL call for its number): 3 ranks timing 0.5 / 1.5 /
+    2.5 s all report 2.5 s."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_max, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(3))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert [v for _, v in res] == [2.5, 2.5, 2.5]

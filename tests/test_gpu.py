@@ -85,6 +85,29 @@ def test_gpu_real_circuits_vs_oracle(p2v, mode, nb):
     assert (otrs[:, off["combined"]: off["combined"] + 2 * r] != 0).all()
 
 
+@pytest.mark.parametrize("nb,lk,mode", [(6, 5, 1), (6, 4, 2), (8, 1, 1), (12, 2, 1), (12, 6, 2)])
+def test_gpu_real_lookup_circuits_vs_oracle(p2v, nb, lk, mode):
+    """valid proofs with a live lookup argument (LookupGate /
+    LookupTableGate blocks on rows, lookup selectors, RE and SLDC polynomials from the
+    prover's witness; 1 or 2 tables, up to a 2^16-entry range table at degree_bits 12) accept
+    on the GPU with C_i and every evalFinalRE value non-zero; perturbed lookup openings,
+    lookup selectors and looked-up wires break the identity.  Statuses and traces equal the
+    oracle's word for word (the oracle's C_i is pinned by test_vanishing_literal.py)."""
+    from support import circuit_shape, trace_offsets
+    from test_real_circuits import _lookup_reject_cases
+    gc = gen_circuit(nb, 4, lk, 1, 28, 16, 0, mode)
+    cases = _lookup_reject_cases(gc)
+    if nb >= 12:
+        cases = cases[:3]
+    sts, otrs = _gpu_vs_oracle(p2v, gc, [c[0] for c in cases])
+    assert sts == [c[1] for c in cases]
+    r, S, Q = circuit_shape(gc.common)
+    off = trace_offsets(r, S, Q)
+    assert (otrs[:, off["combined"]: off["combined"] + 2 * r] != 0).all()
+    nl = len(json.loads(gc.common)["luts"])
+    assert (otrs[:, off["lut_re"]: off["lut_re"] + r * nl] != 0).all()
+
+
 @pytest.mark.parametrize("nb,mode,ext,arities", [(6, 1, 7, (3, 2)), (8, 1, 5, (1, 1, 1, 1)), (6, 2, 6, (3, 1)),
                                                   (8, 1, 7, (3, 2, 1, 1)), (6, 0, 7, (2, 2, 1)), (6, 1, 4, (1, 1, 1)),
                                                   (12, 1, 7, (4, 3, 2))])
@@ -459,12 +482,13 @@ def test_gpu_verify_sharded_single_rank(p2v):
 
 
 def test_gpu_c3_lookup_batch_full_size(p2v):
-    """BASELINE configs[2] shape: 65 536 proofs of the lookup circuit (LookupGate +
-    LookupTableGate, a 256-entry and a 2^16-entry table) at degree_bits 12 in one batch.
+    """BASELINE configs[2] shape: 65 536 proofs of a real lookup circuit (the recursion gate set
+    plus LookupGate / LookupTableGate blocks of a 256-entry and a 2^16-entry table, every lookup
+    term live) at degree_bits 12 in one batch.
     Every valid proof accepts, corrupted lanes reject with the oracle's status, and the
     full trace of sampled lanes (incl. every evalFinalRE value) equals the oracle's."""
     O = oracle()
-    gc = gen_circuit(12, 4, 2)
+    gc = gen_circuit(12, 4, 2, 1, 28, 16, 0, 1)   # real circuit: a live lookup argument (gen.cpp lookup blocks)
     pool = [gc.proof(1, 1), gc.proof(2, 2), gc.proof(1, 5, flags=2)]
     expect = [O.verify_json(gc.common, gc.vkey, p) for p in pool]
     assert expect == [1, 1, 0]
@@ -482,6 +506,62 @@ def test_gpu_c3_lookup_batch_full_size(p2v):
         lanes = np.nonzero(idx == k)[0]
         for lane in (lanes[0], lanes[-1]):
             assert np.array_equal(tr[lane], otr), (k, lane)
+
+
+def test_gpu_c5_shard_one_launch(p2v):
+    """BASELINE configs[4] (C5), one GPU's shard as the bench runs it: ONE launch of 131 072
+    device-resident proofs of the real n = 12 circuit in the 64-proof tiled layout.  Eight
+    distinct valid proofs fill the batch; five corrupted variants (initial leaf -> -1, last step
+    sibling -> -2, first FRI layer -> -3, final polynomial -> False, an opening -> False) sit at
+    lanes spread over the whole batch, incl. the last.  Every other lane accepts (a corruption
+    flips only its own lane), each corrupted lane has the oracle's status, and the full traces of
+    sampled lanes equal the oracle's."""
+    import torch
+    O = oracle()
+    gc = gen_circuit(12, 4, 0, 1, 28, 16, 0, 1)
+    distinct = [gc.proof(1, s) for s in range(1, 9)]
+
+    def leaf(d):
+        d["proof"]["opening_proof"]["query_round_proofs"][3]["initial_trees_proof"]["evals_proofs"][1][0][5] += 1
+
+    def last_sib(d):
+        d["proof"]["opening_proof"]["query_round_proofs"][-1]["steps"][-1]["merkle_proof"]["siblings"][-1]["elements"][3] += 1
+
+    def opening(d):
+        d["proof"]["openings"]["wires"][7][0] += 1
+    variants = [mutate(distinct[0], leaf), mutate(distinct[1], last_sib), gc.proof(1, 21, flags=1),
+                gc.proof(1, 22, flags=2), mutate(distinct[2], opening)]
+    vexp = [O.verify_json(gc.common, gc.vkey, v) for v in variants]
+    assert vexp == [-1, -2, -3, 0, 0]
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    W = vk.info.proof_words
+    B = 131072
+    tile = p2v.tile_proofs(vk.pack_many([distinct[i % 8] for i in range(64)]))   # one 64-proof tile
+    dev = torch.device("cuda", 0)
+    d = torch.from_numpy(tile.view(np.int64)).to(dev).repeat(B // 64)
+    vrows = vk.pack_many(variants)
+    lanes = {}
+    for k in range(len(variants)):
+        for lane in (1 + 26209 * k, 70001 + 9 * k, B - 1 - 2 * k):
+            lanes[lane] = k
+            idx = torch.from_numpy(((lane // 64) * W + np.arange(W, dtype=np.int64)) * 64 + lane % 64).to(dev)
+            d[idx] = torch.from_numpy(vrows[k].view(np.int64)).to(dev)
+    expect = np.ones(B, dtype=np.int8)
+    for lane, k in lanes.items():
+        expect[lane] = vexp[k]
+    res = torch.zeros(B, dtype=torch.int8, device=dev)
+    tw = vk.info.trace_words
+    tr = torch.zeros((B, tw), dtype=torch.int64, device=dev)
+    bv = p2v.BatchVerifier(vk, 0, B)
+    bv.run_device(d.data_ptr(), B, res.data_ptr(), stream=torch.cuda.current_stream(dev).cuda_stream,
+                  trace_ptr=tr.data_ptr(), sync=True, tiled=True)
+    torch.cuda.synchronize(dev)
+    got = res.cpu().numpy()
+    assert np.array_equal(got, expect), np.nonzero(got != expect)[0][:10]
+    otr = {k: O.verify_json(gc.common, gc.vkey, variants[k], trace=True)[1] for k in range(len(variants))}
+    for lane in list(lanes)[::2] + [0, 63, 64, 65535, 65536, B - 2]:
+        ref = otr[lanes[lane]] if lane in lanes else O.verify_json(gc.common, gc.vkey, distinct[lane % 64 % 8], trace=True)[1]
+        assert np.array_equal(tr[lane].cpu().numpy().view(np.uint64), ref), lane
 
 
 @pytest.mark.parametrize("nb,pis,lk,q,pw", [

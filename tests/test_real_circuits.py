@@ -150,3 +150,51 @@ def test_coset_interpolation_row_is_lagrange():
         inv = pow(den, P - 2, P)
         acc = ((acc[0] + t[0] * inv) % P, (acc[1] + t[1] * inv) % P)
     assert (w[35], w[36]) == acc
+
+
+def _lookup_reject_cases(gc):
+    """(proof, expected status, eqs bit or None) on a real lookup circuit: valid proofs, an FRI
+    reject, and openings that only lookup terms read (RE / SLDC at zeta and omega zeta, a
+    lookup selector, the output wire of the first lookup slot) perturbed."""
+    c = json.loads(gc.common)
+    ng, nlp = len(c["selectors_info"]["groups"]), c["num_lookup_polys"]
+    base = gc.proof(1, 3)
+
+    def perturb(key, i, part=0):
+        def f(d):
+            d["proof"]["openings"][key][i][part] = (d["proof"]["openings"][key][i][part] + 1) % P
+        return f
+    return [
+        (base, 1, 3),
+        (gc.proof(2, 4), 1, 3),
+        (gc.proof(1, 4, flags=1), -3, 3),
+        (mutate(base, perturb("lookup_zs", 0)), 0, None),                 # RE, round 0
+        (mutate(base, perturb("lookup_zs", nlp + 3, 1)), 0, None),        # an SLDC column, round 1
+        (mutate(base, perturb("lookup_zs_next", nlp - 1)), 0, None),      # the last SLDC at omega zeta
+        (mutate(base, perturb("constants", ng + 1)), 0, None),            # TransLdc selector
+        (mutate(base, perturb("constants", ng + 4)), 0, None),            # StartEnd_0 selector
+        (mutate(base, perturb("wires", 1)), 0, None),                     # a looked-up output
+    ]
+
+
+@pytest.mark.parametrize("nb,lk,mode", [(6, 5, 1), (6, 4, 2)])
+def test_real_lookup_proofs_accept_and_reject(nb, lk, mode):
+    """Real lookup circuits (LookupGate / LookupTableGate blocks, lookup selectors, RE and
+    SLDC polynomials built by the prover, Plonk/Lookups.hs:45-132): valid proofs accept with
+    C_i != 0, and each perturbed lookup opening breaks the identity."""
+    O = oracle()
+    gc = gen_circuit(nb, 4, lk, 1, 28, 16, 0, mode)
+    c = json.loads(gc.common)
+    assert c["num_lookup_polys"] == 7 and c["num_lookup_selectors"] == 4 + len(c["luts"])
+    assert any(g.startswith("LookupGate") for g in c["gates"]) and any(g.startswith("LookupTableGate") for g in c["gates"])
+    for i, (proof, expect, flags) in enumerate(_lookup_reject_cases(gc)):
+        st, tr = O.verify_json(gc.common, gc.vkey, proof, trace=True)
+        assert st == expect, i
+        fl = _flags(gc, tr)
+        assert (fl & 1 == 0) if flags is None else (fl & 1 == 1), i
+
+
+def test_real_lookup_generator_refuses_a_table_too_large():
+    """A 2^16-entry table needs 2 521 LookupTableGate rows: it does not fit 2^8 rows."""
+    with pytest.raises(RuntimeError, match="do not fit"):
+        gen_circuit(8, 4, 6, 1, 28, 16, 0, 1)

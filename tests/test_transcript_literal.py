@@ -478,8 +478,8 @@ def test_literal_plonk_identity_values_match_oracle_trace(idx):
     case = cases[idx]
     common_b, vkey_b = rd(case["circuit"] + "_common.json.gz"), rd(case["circuit"] + "_vkey.json.gz")
     common = json.loads(common_b)
-    if common["num_lookup_polys"] > 0:
-        pytest.skip("lookup terms are not restated here")
+    if common["num_lookup_polys"] > 0 or case["circuit"].endswith(("_m1", "_m2")):
+        pytest.skip("live gate / lookup terms: the full restatement is tests/test_vanishing_literal.py")
     proof_b = rd(case["name"] + "_proof.json.gz")
     vkey, pwpi = json.loads(vkey_b), json.loads(proof_b)
     ch = proof_challenges(common, vkey, pwpi)
