@@ -23,6 +23,10 @@ module Plonk.VerifierGPU
   , verifyWithCircuit
   , circuitWords
   , proofWords
+    -- * the sub-results the reference's driver prints (src/testmain.hs:54-59), from the GPU trace
+  , proofChallenges
+  , evalCombinedPlonkConstraints
+  , checkCombinedPlonkEquations'
   ) where
 
 import Control.Monad (when, forM_)
@@ -35,8 +39,10 @@ import Foreign.C.String (CString, peekCString)
 import Foreign.C.Types
 import System.IO.Unsafe (unsafePerformIO)
 
-import Algebra.Goldilocks (F, fromF)
-import Algebra.GoldilocksExt (FExt, Ext(..))
+import Algebra.Goldilocks (F, fromF, toF)
+import Algebra.GoldilocksExt (FExt, Ext(..), powExt_)
+import Challenge.FRI (FriChallenges(..))
+import Challenge.Verifier (ProofChallenges(..), LookupDelta(..))
 import Gate.Base (Gate(..), KeccakHash(..))
 import Hash.Digest (Digest(..))
 import Misc.Aux (Log2, fromLog2, Range(..))
@@ -46,6 +52,7 @@ import Types
 -- * C ABI (include/p2v.h)
 
 data P2vCircuit
+data P2vVerifier
 
 foreign import ccall safe "p2v_circuit_from_words"
   c_circuit_from_words :: Ptr Word64 -> CSize -> Ptr (Ptr P2vCircuit) -> IO CInt
@@ -61,6 +68,12 @@ foreign import ccall safe "p2v_verify_batch"
   c_verify_batch :: Ptr P2vCircuit -> Ptr Word64 -> CSize -> Ptr Int8 -> CInt -> IO CInt
 foreign import ccall safe "p2v_verify_batch_devices"
   c_verify_batch_devices :: Ptr P2vCircuit -> Ptr Word64 -> CSize -> Ptr Int8 -> Ptr CInt -> CInt -> CSize -> IO CInt
+foreign import ccall safe "p2v_verifier_create"
+  c_verifier_create :: Ptr P2vCircuit -> CInt -> CSize -> Ptr (Ptr P2vVerifier) -> IO CInt
+foreign import ccall safe "p2v_verifier_free"
+  c_verifier_free :: Ptr P2vVerifier -> IO ()
+foreign import ccall safe "p2v_verifier_run"
+  c_verifier_run :: Ptr P2vVerifier -> Ptr Word64 -> CSize -> Ptr Int8 -> Ptr Word64 -> Ptr () -> Word32 -> IO CInt
 foreign import ccall unsafe "p2v_last_error_message"
   c_last_error :: IO CString
 
@@ -68,9 +81,18 @@ wordsCircuitMagic, wordsProofMagic :: Word64
 wordsCircuitMagic = 0x5032564300000001   -- P2V_WORDS_CIRCUIT_MAGIC
 wordsProofMagic   = 0x5032565000000001   -- P2V_WORDS_PROOF_MAGIC
 
--- | byte offset of @proof_words@ in @p2v_circuit_info@ (12 int32 fields, then int64)
-infoProofWordsOffset :: Int
+-- | byte offsets in @p2v_circuit_info@ (12 int32 fields, then two int64; include/p2v.h)
+infoNumChallengesOffset, infoNumQueryRoundsOffset, infoNumFriStepsOffset, infoHasLookupsOffset :: Int
+infoNumChallengesOffset  = 12
+infoNumQueryRoundsOffset = 16
+infoNumFriStepsOffset    = 20
+infoHasLookupsOffset     = 40
+-- | a buffer that holds p2v_circuit_info (136 bytes in ABI version 1)
+infoBytes :: Int
+infoBytes = 256
+infoProofWordsOffset, infoTraceWordsOffset :: Int
 infoProofWordsOffset = 48
+infoTraceWordsOffset = 56
 
 --------------------------------------------------------------------------------
 -- * Word encoding of the Types.hs values (layout: include/p2v.h)
@@ -209,7 +231,7 @@ statusToBool s = case s of
 verifyWithCircuit :: GpuCircuit -> [Int] -> [ProofWithPublicInputs] -> IO [Bool]
 verifyWithCircuit _ _ [] = pure []
 verifyWithCircuit (GpuCircuit fc) devices proofs = withForeignPtr fc $ \c -> do
-  pw <- allocaBytes 128 $ \info -> do
+  pw <- allocaBytes infoBytes $ \info -> do
     rc <- c_circuit_get_info c info
     when (rc /= 0) $ throwLast "p2v_circuit_get_info"
     peekByteOff info infoProofWordsOffset :: IO Int64
@@ -226,6 +248,82 @@ verifyWithCircuit (GpuCircuit fc) devices proofs = withForeignPtr fc $ \c -> do
                c_verify_batch_devices c buf (fromIntegral n) res dp (fromIntegral k) 0
     when (rc /= 0) $ throwLast "p2v_verify_batch"
     map statusToBool <$> peekArray n res
+
+--------------------------------------------------------------------------------
+-- * Intermediates (the per-proof debug trace, include/p2v.h "debug trace layout")
+
+-- | The packed proof's trace words, with (r, S, Q, has_lookups), computed on GPU 0 by the same
+-- kernels as 'verifyProof'.
+traceOf :: VerifierCircuitData -> ProofWithPublicInputs -> IO ((Int, Int, Int, Bool), [Word64])
+traceOf vkey proof = do
+  GpuCircuit fc <- loadGpuCircuit vkey
+  withForeignPtr fc $ \c -> do
+    (r, s, q, lk, pw, tw) <- allocaBytes infoBytes $ \info -> do
+      rc <- c_circuit_get_info c info
+      when (rc /= 0) $ throwLast "p2v_circuit_get_info"
+      let i32 o = fromIntegral <$> (peekByteOff info o :: IO Int32)
+          i64 o = fromIntegral <$> (peekByteOff info o :: IO Int64)
+      (,,,,,) <$> i32 infoNumChallengesOffset <*> i32 infoNumFriStepsOffset <*> i32 infoNumQueryRoundsOffset
+              <*> ((/= (0 :: Int)) <$> i32 infoHasLookupsOffset) <*> i64 infoProofWordsOffset <*> i64 infoTraceWordsOffset
+    allocaArray pw $ \buf -> allocaArray tw $ \tr -> alloca $ \res -> alloca $ \vp -> do
+      withArrayLen (proofWords proof) $ \m ws -> do
+        rc <- c_pack_proof_words c ws (fromIntegral m) buf
+        when (rc /= 0) $ throwLast "p2v_pack_proof_words"
+      rc <- c_verifier_create c 0 1 vp
+      when (rc /= 0) $ throwLast "p2v_verifier_create"
+      v <- peek vp
+      rc2 <- c_verifier_run v buf 1 res tr nullPtr 0
+      c_verifier_free v
+      when (rc2 /= 0) $ throwLast "p2v_verifier_run"
+      (,) (r, s, q, lk) <$> peekArray tw tr
+
+-- | 'Challenge.Verifier.proofChallenges' (src/Challenge/Verifier.hs:58): same type, the
+-- challenges as the GPU transcript derives them.
+proofChallenges :: CommonCircuitData -> VerifierOnlyCircuitData -> ProofWithPublicInputs -> ProofChallenges
+proofChallenges common vonly proof = unsafePerformIO $ do
+  ((r, s, q, lk), tr) <- traceOf (MkVerifierCircuitData vonly common) proof
+  let at o n = map toF (take n (drop o tr))
+      ext o = MkExt (toF (tr !! o)) (toF (tr !! (o + 1)))
+      oB = 4; oG = oB + r; oA = oG + r; oD = oA + r; oZ = oD + 4 * r
+      oFA = oZ + 2; oFB = oFA + 2; oPow = oFB + 2 * s; oQ = oPow + 1
+      deltas = if lk then [ MkLookupDelta a b c d | i <- [0 .. r - 1], let [a, b, c, d] = at (oD + 4 * i) 4 ] else []
+  pure MkProofChallenges
+    { plonk_betas    = at oB r
+    , plonk_gammas   = at oG r
+    , plonk_alphas   = at oA r
+    , plonk_deltas   = deltas
+    , plonk_zeta     = ext oZ
+    , fri_challenges = MkFriChallenges
+        { fri_alpha         = ext oFA
+        , fri_betas         = [ ext (oFB + 2 * i) | i <- [0 .. s - 1] ]
+        , fri_pow_response  = toF (tr !! oPow)
+        , fri_query_indices = map fromIntegral (take q (drop oQ tr))
+        }
+    }
+{-# NOINLINE proofChallenges #-}
+
+-- | 'Plonk.Vanishing.evalCombinedPlonkConstraints' (src/Plonk/Vanishing.hs:48): C_i(zeta) per
+-- challenge round.  Takes the verifier-only data where the reference takes the challenges:
+-- the GPU derives the challenges itself (the ones 'proofChallenges' returns).
+evalCombinedPlonkConstraints :: CommonCircuitData -> VerifierOnlyCircuitData -> ProofWithPublicInputs -> [FExt]
+evalCombinedPlonkConstraints common vonly proof = fst (combinedAndQuotient common vonly proof)
+
+-- | 'Plonk.Verifier.checkCombinedPlonkEquations'' (src/Plonk/Verifier.hs:35): per round,
+-- Q_i(zeta) (zeta^n - 1) == C_i(zeta), from the GPU's C_i and sum_k zeta^(nk) q_{i,k}.
+checkCombinedPlonkEquations' :: CommonCircuitData -> VerifierOnlyCircuitData -> ProofWithPublicInputs -> [Bool]
+checkCombinedPlonkEquations' common vonly proof =
+  [ qv * (zeta_n - 1) == cv | (qv, cv) <- zip quots combs ]
+  where
+    (combs, quots) = combinedAndQuotient common vonly proof
+    zeta_n = powExt_ (plonk_zeta (proofChallenges common vonly proof)) (circuit_nrows common)
+
+combinedAndQuotient :: CommonCircuitData -> VerifierOnlyCircuitData -> ProofWithPublicInputs -> ([FExt], [FExt])
+combinedAndQuotient common vonly proof = unsafePerformIO $ do
+  ((r, s, q, _), tr) <- traceOf (MkVerifierCircuitData vonly common) proof
+  let ext o = MkExt (toF (tr !! o)) (toF (tr !! (o + 1)))
+      oC = 4 + 3 * r + 4 * r + 4 + 2 * s + 1 + q
+  pure ([ ext (oC + 2 * i) | i <- [0 .. r - 1] ], [ ext (oC + 2 * r + 2 * i) | i <- [0 .. r - 1] ])
+{-# NOINLINE combinedAndQuotient #-}
 
 -- | 'Plonk.Verifier.verifyProof' over a list, on GPU 0.
 verifyProofBatch :: VerifierCircuitData -> [ProofWithPublicInputs] -> IO [Bool]

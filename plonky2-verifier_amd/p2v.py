@@ -669,14 +669,22 @@ def _fri_config_words(fc: dict) -> list:
     return [fc["rate_bits"], fc["cap_height"], fc["proof_of_work_bits"], tag, len(args)] + args + [fc["num_query_rounds"]]
 
 
+# scalar fields in word order, by their JSON keys (Types.hs field names without the aeson-dropped
+# prefix); tests/test_haskell_shim.py holds bindings/haskell/Plonk/VerifierGPU.hs to the same order
+CONFIG_SCALARS = ("num_wires", "num_routed_wires", "num_constants", "use_base_arithmetic_gate", "security_bits",
+                  "num_challenges", "zero_knowledge", "randomize_unused_wires", "max_quotient_degree_factor")
+COMMON_SCALARS_A = ("quotient_degree_factor", "num_gate_constraints", "num_constants", "num_public_inputs")
+COMMON_SCALARS_B = ("num_partial_products", "num_lookup_polys", "num_lookup_selectors")
+OPENING_LISTS = ("constants", "plonk_sigmas", "wires", "plonk_zs", "plonk_zs_next", "partial_products", "quotient_polys",
+                 "lookup_zs", "lookup_zs_next")
+
+
 def circuit_words(common_json: Union[str, bytes], vkey_json: Union[str, bytes]) -> np.ndarray:
     """VerifierCircuitData (Types.hs:220-240) as words, from the JSON files it decodes from."""
     import json
     c, vk = json.loads(common_json), json.loads(vkey_json)
     cfg = c["config"]
-    w = [WORDS_CIRCUIT_MAGIC, cfg["num_wires"], cfg["num_routed_wires"], cfg["num_constants"],
-         int(cfg["use_base_arithmetic_gate"]), cfg["security_bits"], cfg["num_challenges"], int(cfg["zero_knowledge"]),
-         int(cfg["randomize_unused_wires"]), cfg["max_quotient_degree_factor"]]
+    w = [WORDS_CIRCUIT_MAGIC] + [int(cfg[k]) for k in CONFIG_SCALARS]
     w += _fri_config_words(cfg["fri_config"])
     fp = c["fri_params"]
     w += _fri_config_words(fp["config"]) + [int(fp["hiding"]), fp["degree_bits"], len(fp["reduction_arity_bits"])]
@@ -690,9 +698,9 @@ def circuit_words(common_json: Union[str, bytes], vkey_json: Union[str, bytes]) 
         w += [g["start"], g["end"]]
     sv = si.get("selector_vector")
     w += [0] if sv is None else [1, len(sv)] + list(sv)
-    w += [c["quotient_degree_factor"], c["num_gate_constraints"], c["num_constants"], c["num_public_inputs"]]
+    w += [c[k] for k in COMMON_SCALARS_A]
     w += [len(c["k_is"])] + [int(x) % P for x in c["k_is"]]
-    w += [c["num_partial_products"], c["num_lookup_polys"], c["num_lookup_selectors"], len(c["luts"])]
+    w += [c[k] for k in COMMON_SCALARS_B] + [len(c["luts"])]
     for t in c["luts"]:
         w += [len(t)]
         for inp, out in t:
@@ -725,8 +733,7 @@ def proof_words(proof_json: Union[str, bytes]) -> np.ndarray:
     cap(pr["plonk_zs_partial_products_cap"])
     cap(pr["quotient_polys_cap"])
     o = pr["openings"]
-    for k in ("constants", "plonk_sigmas", "wires", "plonk_zs", "plonk_zs_next", "partial_products", "quotient_polys",
-              "lookup_zs", "lookup_zs_next"):
+    for k in OPENING_LISTS:
         exts(o[k])
     fp = pr["opening_proof"]
     w.append(len(fp["commit_phase_merkle_caps"]))
