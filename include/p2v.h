@@ -224,8 +224,9 @@ int  p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n,
  * event wait; the host never blocks).  Chaining two verifiers to each other alternates their
  * phase 1 with the other batch's Merkle / FRI / vanishing work instead of running both batches'
  * phases in lockstep.  prev = NULL removes the link.  Results are unaffected; v and prev must be
- * on the same device, and prev must outlive the link (unlink, or free v first).  Not part of
- * the reference (a batching schedule). */
+ * on the same device.  Freeing either verifier removes its links (the other side then runs
+ * unchained); links and runs may be used from different host threads.  Not part of the
+ * reference (a batching schedule). */
 int  p2v_verifier_chain(p2v_verifier* v, p2v_verifier* prev);
 
 /* Verify n proofs given as ProofWithPublicInputs JSON texts (Types.hs:245-279) in host memory:

@@ -5,7 +5,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <atomic>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -64,6 +66,8 @@ hipError_t upload(DevBuf& b, const std::vector<T>& h) {
   return e;
 }
 
+std::mutex g_chain_mu;   // p2v_verifier_chain links (chain_prev / chain_next of every verifier)
+
 }  // namespace
 
 
@@ -78,8 +82,9 @@ struct p2v_verifier {
   hipEvent_t ev[2 * kNumKernels];   // start/end per kernel
   hipEvent_t dep_p1 = nullptr, dep_side = nullptr, dep_tr = nullptr;
   hipEvent_t p1_done = nullptr;      // recorded on the caller's stream after phase 1 (p2v_verifier_chain)
-  bool p1_recorded = false;
-  p2v_verifier* chain_prev = nullptr;
+  std::atomic<bool> p1_recorded{false};   // read by the workspaces chained to this one, from their host threads
+  p2v_verifier* chain_prev = nullptr;     // chain links: guarded by g_chain_mu
+  std::vector<p2v_verifier*> chain_next;  // workspaces whose chain_prev is this one (cleared when this one is freed)
   hipStream_t side = nullptr;
   float last_ms[kNumKernels] = {0};
   bool timed = false;
@@ -256,6 +261,14 @@ int p2v_device_count(void) {
 
 void p2v_verifier_free(p2v_verifier* v) {
   if (!v) return;
+  {   // unlink: no workspace keeps a pointer to this one, and its own link goes away
+    std::lock_guard<std::mutex> lk(g_chain_mu);
+    for (p2v_verifier* n : v->chain_next) n->chain_prev = nullptr;
+    if (v->chain_prev) {
+      auto& nx = v->chain_prev->chain_next;
+      nx.erase(std::remove(nx.begin(), nx.end(), v), nx.end());
+    }
+  }
   (void)hipSetDevice(v->device);
   for (DevBuf* b : {&v->in, &v->soa, &v->chal, &v->leafdig, &v->mk, &v->fbits, &v->qvals, &v->van, &v->vparts, &v->lutre, &v->res, &v->trace, &v->t_cs, &v->t_kis,
                     &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit, &v->t_rin, &v->t_rout, &v->t_roff, &v->t_rch, &v->t_pbase, &v->lutpart, &v->j_blob, &v->j_offs, &v->j_skel, &v->j_tok, &v->j_ok,
@@ -274,7 +287,13 @@ void p2v_verifier_free(p2v_verifier* v) {
 int p2v_verifier_chain(p2v_verifier* v, p2v_verifier* prev) {
   if (!v) return fail(P2V_E_ARG, "null verifier");
   if (prev && prev->device != v->device) return fail(P2V_E_ARG, "p2v_verifier_chain: verifiers on different devices");
+  std::lock_guard<std::mutex> lk(g_chain_mu);
+  if (v->chain_prev) {
+    auto& nx = v->chain_prev->chain_next;
+    nx.erase(std::remove(nx.begin(), nx.end(), v), nx.end());
+  }
   v->chain_prev = prev;
+  if (prev) prev->chain_next.push_back(v);
   return P2V_OK;
 }
 
@@ -532,7 +551,11 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   const int nt_blocks = (tl * d.B + 255) / 256;
   const int leaf_units = d.Q * d.T * NPB;
   // staggered workspaces (p2v_verifier_chain): phase 1 after the linked workspace's latest one
-  if (v->chain_prev && v->chain_prev->p1_recorded) HCK(hipStreamWaitEvent(st, v->chain_prev->p1_done, 0));
+  {
+    std::lock_guard<std::mutex> lk(g_chain_mu);   // the linked workspace cannot be freed meanwhile
+    if (v->chain_prev && v->chain_prev->p1_recorded.load(std::memory_order_acquire))
+      HCK(hipStreamWaitEvent(st, v->chain_prev->p1_done, 0));
+  }
   if (!v->split_phase1 || sd == st) {
     T0(1, st);
     k_phase1<<<nt_blocks + (leaf_units + 3) / 4, 256, 0, st>>>(d, nt_blocks, tl);
@@ -557,7 +580,7 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     HCK(hipStreamWaitEvent(st, v->dep_tr, 0));   // k_merkle reads the query indices
   }
   HCK(hipEventRecord(v->p1_done, st));   // k_merkle's inputs are complete on st here in both forms
-  v->p1_recorded = true;
+  v->p1_recorded.store(true, std::memory_order_release);
   // phase 2: Merkle paths on the main stream; FRI queries and the vanishing kernel (few,
   // long-latency waves) on the side stream, concurrently
   // k_fri first: it needs only phase 1 and is the shorter chain, so the vanishing kernels

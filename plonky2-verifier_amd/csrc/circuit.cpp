@@ -125,12 +125,21 @@ static void digest_of(const JVal& d, uint64_t* out) {   // Hash/Digest.hs:40-44
 // expandReductionStrategy starts from degree_bits (Plonk/FRI.hs:337-354, :378)
 enum { STRAT_FIXED = 0, STRAT_CONSTANT_ARITY_BITS = 1, STRAT_MIN_SIZE = 2 };   // FriReductionStrategy, Types.hs:128-131
 static void expand_strategy(Circuit& C, int tag, const std::vector<int64_t>& a) {
+  // bounds first: the step list is expanded before finalize_circuit validates the
+  // sizes, so an absurd degree_bits / final_poly_bits must not drive the expansion loop
+  constexpr int kMaxSteps = 64;
+  if (C.degree_bits < 0 || C.degree_bits > 64) throw CircuitError("unsupported FRI sizes");
+  for (int64_t x : a) if (x < -64 || x > 64) throw CircuitError("reduction strategy argument out of range");
   if (tag == STRAT_CONSTANT_ARITY_BITS) {
     if (a.size() != 2) throw ParseError("ConstantArityBits: expecting [arity_bits, final_poly_bits]");
     const int ab = (int)a[0], f = (int)a[1];
     if (ab <= 0 && C.degree_bits > f) throw CircuitError("reduction strategy does not terminate (arity_bits <= 0)");
-    for (int logn = C.degree_bits; logn > f; logn -= ab) C.arities.push_back(ab);
+    for (int logn = C.degree_bits; logn > f; logn -= ab) {
+      if ((int)C.arities.size() == kMaxSteps) throw CircuitError("reduction strategy: too many FRI steps");
+      C.arities.push_back(ab);
+    }
   } else if (tag == STRAT_FIXED) {
+    if (a.size() > (size_t)kMaxSteps) throw CircuitError("reduction strategy: too many FRI steps");
     for (int64_t x : a) C.arities.push_back((int)x);
   } else if (tag == STRAT_MIN_SIZE) {
     if (a.size() > 1) throw ParseError("MinSize: expecting an optional max arity");
@@ -160,28 +169,28 @@ Circuit parse_circuit(const JVal& common, const JVal& vkey, uint32_t ext) {
   Circuit C;
   C.ext = ext;
   const JVal& cfg = common.at("config");
-  C.num_wires = (int)j_int(cfg.at("num_wires"));
-  C.num_routed = (int)j_int(cfg.at("num_routed_wires"));
-  C.num_gate_consts = (int)j_int(cfg.at("num_constants"));
+  C.num_wires = j_i32(cfg.at("num_wires"));
+  C.num_routed = j_i32(cfg.at("num_routed_wires"));
+  C.num_gate_consts = j_i32(cfg.at("num_constants"));
   (void)j_bool(cfg.at("use_base_arithmetic_gate"));
   (void)j_int(cfg.at("security_bits"));
-  C.r = (int)j_int(cfg.at("num_challenges"));
+  C.r = j_i32(cfg.at("num_challenges"));
   (void)j_bool(cfg.at("zero_knowledge"));
   (void)j_bool(cfg.at("randomize_unused_wires"));
-  C.max_qdf = (int)j_int(cfg.at("max_quotient_degree_factor"));
+  C.max_qdf = j_i32(cfg.at("max_quotient_degree_factor"));
   const JVal& fc = cfg.at("fri_config");
-  C.rate_bits = (int)j_int(fc.at("rate_bits"));
-  C.cap_height = (int)j_int(fc.at("cap_height"));
-  C.pow_bits = (int)j_int(fc.at("proof_of_work_bits"));
-  C.num_queries = (int)j_int(fc.at("num_query_rounds"));
+  C.rate_bits = j_i32(fc.at("rate_bits"));
+  C.cap_height = j_i32(fc.at("cap_height"));
+  C.pow_bits = j_i32(fc.at("proof_of_work_bits"));
+  C.num_queries = j_i32(fc.at("num_query_rounds"));
   const JVal& rs = fc.at("reduction_strategy");
   if (rs.kind != JVal::Obj || rs.keys.size() != 1) throw ParseError("reduction_strategy: expecting a singleton object");
   const JVal& fp = common.at("fri_params");
   C.hiding = j_bool(fp.at("hiding"));
-  C.degree_bits = (int)j_int(fp.at("degree_bits"));
-  for (const auto& x : fp.at("reduction_arity_bits").arr()) C.params_arities.push_back((int)j_int(x));
+  C.degree_bits = j_i32(fp.at("degree_bits"));
+  for (const auto& x : fp.at("reduction_arity_bits").arr()) C.params_arities.push_back(j_i32(x));
   (void)fp.at("config");
-  C.lde_bits = C.degree_bits + C.rate_bits;
+  C.lde_bits = (int)std::max<int64_t>(INT32_MIN, std::min<int64_t>(INT32_MAX, (int64_t)C.degree_bits + C.rate_bits));   // range-checked in finalize_circuit
   if (rs.keys[0] == "ConstantArityBits") {
     const auto& ab = rs.items[0].arr();
     if (ab.size() != 2) throw ParseError("ConstantArityBits: expecting [arity_bits, final_poly_bits]");
@@ -204,16 +213,16 @@ Circuit parse_circuit(const JVal& common, const JVal& vkey, uint32_t ext) {
     C.gates.push_back(parse_gate_string(g.text));
   }
   const JVal& si = common.at("selectors_info");
-  for (const auto& x : si.at("selector_indices").arr()) C.sel_idx.push_back((int)j_int(x));
-  for (const auto& g : si.at("groups").arr()) { C.grp_start.push_back((int)j_int(g.at("start"))); C.grp_end.push_back((int)j_int(g.at("end"))); }
-  C.qdf = (int)j_int(common.at("quotient_degree_factor"));
-  C.num_gate_constraints = (int)j_int(common.at("num_gate_constraints"));
-  C.num_constants = (int)j_int(common.at("num_constants"));
-  C.num_pis = (int)j_int(common.at("num_public_inputs"));
+  for (const auto& x : si.at("selector_indices").arr()) C.sel_idx.push_back(j_i32(x));
+  for (const auto& g : si.at("groups").arr()) { C.grp_start.push_back(j_i32(g.at("start"))); C.grp_end.push_back(j_i32(g.at("end"))); }
+  C.qdf = j_i32(common.at("quotient_degree_factor"));
+  C.num_gate_constraints = j_i32(common.at("num_gate_constraints"));
+  C.num_constants = j_i32(common.at("num_constants"));
+  C.num_pis = j_i32(common.at("num_public_inputs"));
   for (const auto& x : common.at("k_is").arr()) C.k_is.push_back(j_field(x));
-  C.npp = (int)j_int(common.at("num_partial_products"));
-  C.nlp = (int)j_int(common.at("num_lookup_polys"));
-  C.nls = (int)j_int(common.at("num_lookup_selectors"));
+  C.npp = j_i32(common.at("num_partial_products"));
+  C.nlp = j_i32(common.at("num_lookup_polys"));
+  C.nls = j_i32(common.at("num_lookup_selectors"));
   for (const auto& t : common.at("luts").arr()) {
     std::vector<uint64_t> in, out;
     for (const auto& e : t.arr()) {
@@ -437,6 +446,11 @@ struct WordReader {
   const uint64_t* w; size_t n; size_t i = 0;
   uint64_t u(const char* what) { if (i >= n) throw ParseError(std::string("words: truncated at ") + what); return w[i++]; }
   int64_t s(const char* what) { return (int64_t)u(what); }
+  int i32(const char* what) {   // an Int stored as int here: out-of-range values are rejected, not truncated
+    const int64_t x = s(what);
+    if (x < INT32_MIN || x > INT32_MAX) throw ParseError(std::string("words: Int out of range in ") + what);
+    return (int)x;
+  }
   int64_t len(const char* what) {
     const int64_t k = s(what);
     if (k < 0 || (uint64_t)k > n - i) throw ParseError(std::string("words: bad list length of ") + what);
@@ -448,12 +462,12 @@ struct WordReader {
 };
 
 void read_fri_config(WordReader& R, int& rate, int& cap, int& pow, int& tag, std::vector<int64_t>& args, int& nq) {
-  rate = (int)R.s("fri_rate_bits"); cap = (int)R.s("fri_cap_height"); pow = (int)R.s("fri_proof_of_work_bits");
-  tag = (int)R.s("fri_reduction_strategy");
+  rate = R.i32("fri_rate_bits"); cap = R.i32("fri_cap_height"); pow = R.i32("fri_proof_of_work_bits");
+  tag = R.i32("fri_reduction_strategy");
   const int64_t k = R.len("reduction strategy fields");
   args.clear();
   for (int64_t i = 0; i < k; i++) args.push_back(R.s("reduction strategy field"));
-  nq = (int)R.s("fri_num_query_rounds");
+  nq = R.i32("fri_num_query_rounds");
 }
 
 const char* gate_name(int k) {
@@ -470,24 +484,24 @@ Circuit parse_circuit_words(const uint64_t* w, size_t n, uint32_t ext) {
   Circuit C;
   C.ext = ext;
   // CircuitConfig (Types.hs:73-84)
-  C.num_wires = (int)R.s("config_num_wires");
-  C.num_routed = (int)R.s("config_num_routed_wires");
-  C.num_gate_consts = (int)R.s("config_num_constants");
+  C.num_wires = R.i32("config_num_wires");
+  C.num_routed = R.i32("config_num_routed_wires");
+  C.num_gate_consts = R.i32("config_num_constants");
   (void)R.b("config_use_base_arithmetic_gate");
   (void)R.s("config_security_bits");
-  C.r = (int)R.s("config_num_challenges");
+  C.r = R.i32("config_num_challenges");
   (void)R.b("config_zero_knowledge");
   (void)R.b("config_randomize_unused_wires");
-  C.max_qdf = (int)R.s("config_max_quotient_degree_factor");
+  C.max_qdf = R.i32("config_max_quotient_degree_factor");
   int tag = 0, tag2 = 0, d0, d1, d2, d3;
   std::vector<int64_t> sargs, sargs2;
   read_fri_config(R, C.rate_bits, C.cap_height, C.pow_bits, tag, sargs, C.num_queries);
   // FriParams (Types.hs:151-157): its own FriConfig copy, hiding, degree_bits, arity bits
   read_fri_config(R, d0, d1, d2, tag2, sargs2, d3);
   C.hiding = R.b("fri_hiding");
-  C.degree_bits = (int)R.s("fri_degree_bits");
-  for (int64_t k = R.len("fri_reduction_arity_bits"); k > 0; k--) C.params_arities.push_back((int)R.s("fri_reduction_arity_bits"));
-  C.lde_bits = C.degree_bits + C.rate_bits;
+  C.degree_bits = R.i32("fri_degree_bits");
+  for (int64_t k = R.len("fri_reduction_arity_bits"); k > 0; k--) C.params_arities.push_back(R.i32("fri_reduction_arity_bits"));
+  C.lde_bits = (int)std::max<int64_t>(INT32_MIN, std::min<int64_t>(INT32_MAX, (int64_t)C.degree_bits + C.rate_bits));   // range-checked in finalize_circuit
   fri_steps(C, tag, sargs);
   // gates (Gate/Base.hs:27-45)
   for (int64_t k = R.len("circuit_gates"); k > 0; k--) {
@@ -526,17 +540,17 @@ Circuit parse_circuit_words(const uint64_t* w, size_t n, uint32_t ext) {
     C.gates.push_back(std::move(g));
   }
   // SelectorsInfo (Types.hs:90-95)
-  for (int64_t k = R.len("selector_indices"); k > 0; k--) C.sel_idx.push_back((int)R.s("selector index"));
-  for (int64_t k = R.len("selector_groups"); k > 0; k--) { C.grp_start.push_back((int)R.s("range_start")); C.grp_end.push_back((int)R.s("range_end")); }
+  for (int64_t k = R.len("selector_indices"); k > 0; k--) C.sel_idx.push_back(R.i32("selector index"));
+  for (int64_t k = R.len("selector_groups"); k > 0; k--) { C.grp_start.push_back(R.i32("range_start")); C.grp_end.push_back(R.i32("range_end")); }
   if (R.b("selector_vector present")) for (int64_t k = R.len("selector_vector"); k > 0; k--) (void)R.s("selector_vector");
-  C.qdf = (int)R.s("circuit_quotient_degree_factor");
-  C.num_gate_constraints = (int)R.s("circuit_num_gate_constraints");
-  C.num_constants = (int)R.s("circuit_num_constants");
-  C.num_pis = (int)R.s("circuit_num_public_inputs");
+  C.qdf = R.i32("circuit_quotient_degree_factor");
+  C.num_gate_constraints = R.i32("circuit_num_gate_constraints");
+  C.num_constants = R.i32("circuit_num_constants");
+  C.num_pis = R.i32("circuit_num_public_inputs");
   for (int64_t k = R.len("circuit_k_is"); k > 0; k--) C.k_is.push_back(R.f("k_i"));
-  C.npp = (int)R.s("circuit_num_partial_products");
-  C.nlp = (int)R.s("circuit_num_lookup_polys");
-  C.nls = (int)R.s("circuit_num_lookup_selectors");
+  C.npp = R.i32("circuit_num_partial_products");
+  C.nlp = R.i32("circuit_num_lookup_polys");
+  C.nls = R.i32("circuit_num_lookup_selectors");
   for (int64_t k = R.len("circuit_luts"); k > 0; k--) {   // LookupTable = [(Word64, Word64)], Types.hs:28-33
     std::vector<uint64_t> in, out;
     for (int64_t m = R.len("lookup table"); m > 0; m--) { in.push_back(R.u("lut input") % gl::P); out.push_back(R.u("lut output") % gl::P); }

@@ -146,12 +146,10 @@ __device__ __forceinline__ uint64_t mul_nc_dev_v(uint64_t a, uint64_t b) {
   return ((uint64_t)rh2 << 32) | rl2;
   }
 }
-// the general-purpose multiply (FRI, vanishing, gates): the branch-free one-fix-up form
-// (P2V_GENERAL_MUL selects another form for measurement / fault isolation builds)
-#ifndef P2V_GENERAL_MUL
-#define P2V_GENERAL_MUL 1
-#endif
-__device__ __forceinline__ uint64_t mul_nc_dev(uint64_t a, uint64_t b) { return mul_nc_dev_v<P2V_GENERAL_MUL>(a, b); }
+// the general-purpose multiply (FRI, vanishing, gates): the branch-free one-fix-up form.  (The
+// round-1 build option that put the branch form V = 2 here is gone: it was slower, and the one
+// fault seen under it was never reproduced; V = 2 stays the S-box's form)
+__device__ __forceinline__ uint64_t mul_nc_dev(uint64_t a, uint64_t b) { return mul_nc_dev_v<1>(a, b); }
 #endif
 
 GL_HD void mul128(uint64_t a, uint64_t b, uint64_t& hi, uint64_t& lo) {

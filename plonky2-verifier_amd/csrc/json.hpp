@@ -155,6 +155,13 @@ inline int64_t j_int(const JVal& v) {
   }
   return std::stoll(v.text);
 }
+// an Int field this build stores as int: values outside int32 are rejected, never truncated
+inline int j_i32(const JVal& v) {
+  if (v.kind == JVal::Num && v.text.size() > 11) throw ParseError("Int field out of range");
+  const int64_t x = j_int(v);
+  if (x < INT32_MIN || x > INT32_MAX) throw ParseError("Int field out of range");
+  return (int)x;
+}
 inline uint64_t j_word64_mod_p(const JVal& v) {   // Word64 then toF (Types.hs:30-35)
   if (v.kind != JVal::Num || v.text.empty() || v.text[0] == '-') throw ParseError("expected Word64");
   unsigned __int128 acc = 0;

@@ -1,12 +1,11 @@
 #!/bin/bash
 # Measurement / isolation builds of libp2v with extra compile flags, loaded through P2V_LIB:
 #   variants/build.sh <name> "<flags>"   ->   variants/libp2v_<name>.so
-#   mul2:  -DP2V_GENERAL_MUL=2   (branch form of the general multiply)
 #   pm:    -DP2V_PROOF_MAJOR=1   (kernels read the proof-major batch in place, no k_transpose)
 set -e
 cd "$(dirname "$0")/.."
 NAME=$1; EXTRA=$2
-F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result $EXTRA"
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -Werror=inline-asm $EXTRA"
 mkdir -p variants/build_$NAME
 for t in kernels vanish json_pack; do /opt/rocm/bin/hipcc $F -c -o variants/build_$NAME/$t.o csrc/$t.hip & done
 /opt/rocm/bin/hipcc $F -x hip -c -o variants/build_$NAME/api.o csrc/api.cpp &

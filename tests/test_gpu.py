@@ -277,6 +277,13 @@ def test_gpu_chained_workspaces(p2v):
     for bv in bvs:
         bv.chain(None)
     assert np.array_equal(bvs[0].run(batches[1]), want[1])
+    # freeing the linked-to workspace first removes the link: the other one runs unchained
+    import ctypes
+    bvs[1].chain(bvs[0])
+    assert np.array_equal(bvs[1].run(batches[2]), want[2])
+    p2v.lib().p2v_verifier_free(bvs[0]._h)
+    bvs[0]._h = ctypes.c_void_p()
+    assert np.array_equal(bvs[1].run(batches[3]), want[3])
 
 
 def _number_paths(d, path=()):

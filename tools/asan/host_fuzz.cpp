@@ -50,6 +50,33 @@ int main(int argc, char** argv) {
   if (out != ref) { fprintf(stderr, "words path != JSON path\n"); return 1; }
   ProofTemplate T;
   if (!T.build(C, proof.data(), proof.size(), out.data()) || out != ref) { fprintf(stderr, "template build\n"); return 1; }
+  // huge Int fields must be rejected before the reduction strategy is expanded (no
+  // unbounded allocation, no truncating casts).  Word layout with ConstantArityBits: [9] config
+  // scalars, FriConfig at 10 (tag 13, 2 args at 15 16), FriParams' FriConfig at 18, degree_bits 27.
+  if (cw.size() / 8 < 28 || ((const uint64_t*)cw.data())[13] != 1 || ((const uint64_t*)cw.data())[14] != 2) {
+    fprintf(stderr, "unexpected circuit word layout\n"); return 1;
+  }
+  struct Crafted { int idx[3]; uint64_t val[3]; int want; const char* what; };
+  const Crafted crafted[] = {
+    {{27, 15, 16}, {0x7FFFFFFFull, 1, (uint64_t)-(int64_t)1000000000}, 3, "degree_bits 2^31-1, arity 1, final_poly_bits -1e9"},
+    {{27, -1, -1}, {1ull << 40, 0, 0}, 2, "degree_bits 2^40 (past int)"},
+    {{1, -1, -1}, {(uint64_t)-(int64_t)(1ll << 35), 0, 0}, 2, "num_wires -2^35"},
+    {{16, -1, -1}, {(uint64_t)-(int64_t)(1ll << 33), 0, 0}, 3, "final_poly_bits -2^33"},
+  };
+  for (const auto& k : crafted) {
+    std::string x = cw;
+    for (int j = 0; j < 3; j++) if (k.idx[j] >= 0) ((uint64_t*)&x[0])[k.idx[j]] = k.val[j];
+    const int got = guarded([&] { Circuit X = parse_circuit_words((const uint64_t*)x.data(), x.size() / 8); });
+    if (got != k.want) { fprintf(stderr, "crafted words (%s): class %d, expected %d\n", k.what, got, k.want); return 1; }
+  }
+  {
+    std::string j = common;
+    const size_t at = j.find("\"degree_bits\":");
+    if (at == std::string::npos) { fprintf(stderr, "no degree_bits\n"); return 1; }
+    j.insert(at + 14, "2147483647000");   // a number past int: rejected, not truncated
+    const int got = guarded([&] { Circuit X = parse_circuit(parse_json(j.data(), j.size()), parse_json(vkey.data(), vkey.size())); });
+    if (got != 2) { fprintf(stderr, "crafted JSON degree_bits: class %d, expected 2 (parse)\n", got); return 1; }
+  }
   std::mt19937_64 rng(12345);
   int counts[5] = {0, 0, 0, 0, 0};
   for (int it = 0; it < iters; it++) {
