@@ -29,7 +29,8 @@ module Plonk.VerifierGPU
   , checkCombinedPlonkEquations'
   ) where
 
-import Control.Monad (when, forM_)
+import Control.Exception (finally)
+import Control.Monad (when, forM, forM_)
 import Data.Bits ((.&.))
 import Data.Char (ord)
 import Data.Int (Int8, Int32, Int64)
@@ -68,6 +69,12 @@ foreign import ccall safe "p2v_verify_batch"
   c_verify_batch :: Ptr P2vCircuit -> Ptr Word64 -> CSize -> Ptr Int8 -> CInt -> IO CInt
 foreign import ccall safe "p2v_verify_batch_devices"
   c_verify_batch_devices :: Ptr P2vCircuit -> Ptr Word64 -> CSize -> Ptr Int8 -> Ptr CInt -> CInt -> CSize -> IO CInt
+foreign import ccall safe "p2v_proof_shape_words"
+  c_proof_shape_words :: Ptr Word64 -> CSize -> Ptr CInt -> Ptr CInt -> IO CInt
+foreign import ccall safe "p2v_circuit_shape_variant"
+  c_circuit_shape_variant :: Ptr P2vCircuit -> CInt -> CInt -> Ptr (Ptr P2vCircuit) -> IO CInt
+foreign import ccall safe "p2v_circuit_free"
+  c_circuit_free_now :: Ptr P2vCircuit -> IO ()
 foreign import ccall safe "p2v_verifier_create"
   c_verifier_create :: Ptr P2vCircuit -> CInt -> CSize -> Ptr (Ptr P2vVerifier) -> IO CInt
 foreign import ccall safe "p2v_verifier_free"
@@ -227,27 +234,64 @@ statusToBool s = case s of
   (-4) -> error "folding step: reduction strategy incompatibility"
   k    -> error ("p2v status " ++ show k)
 
--- | Verify a batch on the given devices (one shard per entry, p2v_verify_batch_devices).
+-- | p2v_circuit_get_info's proof_words
+infoProofWords :: Ptr P2vCircuit -> IO Int64
+infoProofWords c = allocaBytes infoBytes $ \info -> do
+  rc <- c_circuit_get_info c info
+  when (rc /= 0) $ throwLast "p2v_circuit_get_info"
+  peekByteOff info infoProofWordsOffset :: IO Int64
+
+-- | P2V_E_SHAPE: the proof's lengths do not fit the circuit's packed layout
+eShape :: CInt
+eShape = -3
+
+-- | Verify a batch on the given devices (one shard per entry, p2v_verify_batch_devices).  A proof
+-- with another number of public inputs or final-polynomial coefficients than the circuit implies
+-- is verified on its own against the circuit's shape variant for those lengths
+-- (p2v_circuit_shape_variant): the reference reads both lists at any length
+-- (src/Hash/Sponge.hs:26-31, src/Plonk/FRI.hs:325-327).
 verifyWithCircuit :: GpuCircuit -> [Int] -> [ProofWithPublicInputs] -> IO [Bool]
 verifyWithCircuit _ _ [] = pure []
 verifyWithCircuit (GpuCircuit fc) devices proofs = withForeignPtr fc $ \c -> do
-  pw <- allocaBytes infoBytes $ \info -> do
-    rc <- c_circuit_get_info c info
-    when (rc /= 0) $ throwLast "p2v_circuit_get_info"
-    peekByteOff info infoProofWordsOffset :: IO Int64
+  pw <- infoProofWords c
   let n = length proofs
       w = fromIntegral pw
   allocaArray (n * w) $ \buf -> allocaArray n $ \res -> do
-    forM_ (zip [0 ..] proofs) $ \(i, p) ->
+    codes <- forM (zip [0 ..] proofs) $ \(i, p) ->
       withArrayLen (proofWords p) $ \m ws -> do
-        rc <- c_pack_proof_words c ws (fromIntegral m) (buf `advancePtr` (i * w))
-        when (rc /= 0) $ throwLast "p2v_pack_proof_words"
+        let row = buf `advancePtr` (i * w)
+        rc <- c_pack_proof_words c ws (fromIntegral m) row
+        when (rc /= 0 && rc /= eShape) $ throwLast "p2v_pack_proof_words"
+        when (rc == eShape) $ fillBytes row 0 (w * 8)   -- verified below through its variant
+        pure rc
     rc <- case devices of
       [d] -> c_verify_batch c buf (fromIntegral n) res (fromIntegral d)
       ds  -> withArrayLen (map fromIntegral ds) $ \k dp ->
                c_verify_batch_devices c buf (fromIntegral n) res dp (fromIntegral k) 0
     when (rc /= 0) $ throwLast "p2v_verify_batch"
-    map statusToBool <$> peekArray n res
+    sts <- peekArray n res
+    forM (zip3 proofs codes sts) $ \(p, code, st) ->
+      statusToBool <$> (if code == eShape then verifyShapeVariant c (head (devices ++ [0])) p else pure st)
+
+-- | One proof whose public-input / final-polynomial lengths differ from the circuit's.
+verifyShapeVariant :: Ptr P2vCircuit -> Int -> ProofWithPublicInputs -> IO Int8
+verifyShapeVariant c dev p = withArrayLen (proofWords p) $ \m ws ->
+  alloca $ \np -> alloca $ \nf -> alloca $ \out -> do
+    rc <- c_proof_shape_words ws (fromIntegral m) np nf
+    when (rc /= 0) $ throwLast "p2v_proof_shape_words"
+    a <- peek np
+    b <- peek nf
+    rc2 <- c_circuit_shape_variant c a b out
+    when (rc2 /= 0) $ throwLast "p2v_circuit_shape_variant"
+    v <- peek out
+    flip finally (c_circuit_free_now v) $ do
+      pwv <- infoProofWords v
+      allocaArray (fromIntegral pwv) $ \buf -> alloca $ \r -> do
+        rc3 <- c_pack_proof_words v ws (fromIntegral m) buf
+        when (rc3 /= 0) $ throwLast "p2v_pack_proof_words"
+        rc4 <- c_verify_batch v buf 1 r (fromIntegral dev)
+        when (rc4 /= 0) $ throwLast "p2v_verify_batch"
+        peek r
 
 --------------------------------------------------------------------------------
 -- * Intermediates (the per-proof debug trace, include/p2v.h "debug trace layout")

@@ -183,6 +183,21 @@ int  p2v_pack_proof_words(const p2v_circuit* c, const uint64_t* words, size_t n,
  * input count the circuit does not imply.  Parity unpinned (no binary fixture offline). */
 int  p2v_pack_proof_bytes(const p2v_circuit* c, const uint8_t* bytes, size_t n, uint64_t* dst);
 
+/* ---- shape variants --------------------------------------------------------------------
+ * The reference reads public_inputs and final_poly.coeffs at whatever length a proof carries:
+ * the public inputs enter only through their sponge (Hash/Sponge.hs:26-31, Challenge/
+ * Verifier.hs:68, Plonk/Vanishing.hs:86), the final polynomial through its absorb and its
+ * evaluation (Challenge/FRI.hs:83, Plonk/FRI.hs:325-327).  A proof whose lengths differ from
+ * the circuit's (num_public_inputs; 2^(degree_bits - sum arity_bits)) fails to pack with
+ * P2V_E_SHAPE; p2v_proof_shape_* read its two lengths and p2v_circuit_shape_variant derives the
+ * circuit whose packed layout has them (same circuit otherwise; free with p2v_circuit_free), so
+ * the proof is verified on the GPU with the reference's outcome (False in practice: the
+ * transcript diverges).  Limits: up to 2^20 public inputs / coefficients (else P2V_E_SHAPE).
+ * Every other length mismatch is an `error` in the reference too and stays P2V_E_SHAPE. */
+int  p2v_proof_shape_json(const char* proof_json, size_t len, int* num_public_inputs, int* final_poly_len);
+int  p2v_proof_shape_words(const uint64_t* words, size_t n, int* num_public_inputs, int* final_poly_len);
+int  p2v_circuit_shape_variant(const p2v_circuit* c, int num_public_inputs, int final_poly_len, p2v_circuit** out);
+
 /* ---- verification (GPU) ------------------------------------------------------------ */
 #define P2V_FLAG_INPUT_DEVICE  1u  /* `proofs` is a device pointer on the verifier's device  */
 #define P2V_FLAG_RESULT_DEVICE 2u  /* `results` (and trace) are device pointers              */

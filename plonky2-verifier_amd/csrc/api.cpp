@@ -205,6 +205,33 @@ int p2v_pack_proof_json(const p2v_circuit* pc, const char* proof_json, size_t le
   catch (const std::exception& e) { return fail(P2V_E_PARSE, e.what()); }
 }
 
+int p2v_proof_shape_json(const char* proof_json, size_t len, int* num_public_inputs, int* final_poly_len) {
+  if (!proof_json || !num_public_inputs || !final_poly_len) return fail(P2V_E_ARG, "null argument");
+  try {
+    proof_shape_json(parse_json(proof_json, len), *num_public_inputs, *final_poly_len);
+    return P2V_OK;
+  } catch (const std::exception& e) { return fail(P2V_E_PARSE, e.what()); }
+}
+
+int p2v_proof_shape_words(const uint64_t* words, size_t n, int* num_public_inputs, int* final_poly_len) {
+  if (!words || !num_public_inputs || !final_poly_len) return fail(P2V_E_ARG, "null argument");
+  try {
+    proof_shape_words(words, n, *num_public_inputs, *final_poly_len);
+    return P2V_OK;
+  } catch (const std::exception& e) { return fail(P2V_E_PARSE, e.what()); }
+}
+
+int p2v_circuit_shape_variant(const p2v_circuit* pc, int num_public_inputs, int final_poly_len, p2v_circuit** out) {
+  if (!pc || !out) return fail(P2V_E_ARG, "null argument");
+  *out = nullptr;
+  try {
+    auto* v = new p2v_circuit{circuit_shape_variant(pc->c, num_public_inputs, final_poly_len)};
+    *out = v;
+    return P2V_OK;
+  } catch (const CircuitError& e) { return fail(P2V_E_SHAPE, e.what()); }
+  catch (const std::exception& e) { return fail(P2V_E_SHAPE, e.what()); }
+}
+
 int p2v_pack_proofs_json(const p2v_circuit* pc, const char* const* jsons, const size_t* lens, size_t n, uint64_t* dst,
                          int32_t* codes, int threads) {
   if (!pc || (n && (!jsons || !lens || !dst || !codes))) return fail(P2V_E_ARG, "null argument");

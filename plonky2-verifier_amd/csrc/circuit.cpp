@@ -288,7 +288,7 @@ static void finalize_circuit(Circuit& C) {
   int sum_a = 0; for (int a : C.arities) { if (a <= 0 || a > 8) throw CircuitError("unsupported FRI arity"); sum_a += a; }
   if (sum_a > C.degree_bits) throw CircuitError("reduction strategy folds below degree 1");
   if (C.arities.size() > 8) throw CircuitError("more than 8 FRI steps");
-  C.final_len = 1 << (C.degree_bits - sum_a);
+  C.final_len = C.final_len_override >= 0 ? C.final_len_override : 1 << (C.degree_bits - sum_a);
   C.oracle_width[0] = C.num_constants + C.num_routed;
   C.oracle_width[1] = C.num_wires;
   C.oracle_width[2] = C.r * (1 + C.npp + C.nlp);
@@ -300,6 +300,7 @@ static void finalize_circuit(Circuit& C) {
   C.noop_leaves = (C.ext & P2V_EXT_HASH_OR_NOOP) != 0;
   C.depth0 = C.lde_bits - C.cap_height;
   if (C.depth0 < 0) throw CircuitError("cap_height exceeds the LDE size");
+  C.step_depth.clear();
   { int logn = C.lde_bits; for (int a : C.arities) { logn -= a; C.step_depth.push_back(std::max(0, logn - C.cap_height)); } }
   // term counts before the gate terms (Vanishing.hs:67-111, Lookups.hs:73-132)
   {
@@ -319,6 +320,7 @@ static void finalize_circuit(Circuit& C) {
     C.alpha_base_gates = C.r + C.r * C.n_pp_terms_per_round + (nluts > 0 ? C.r * C.n_lookup_terms_per_round : 0);
   }
   // ---------------------------------------------------------------- layout
+  C.L = Layout{};
   Layout& L = C.L;
   int64_t w = 0;
   L.pis = w; w += C.num_pis;
@@ -433,6 +435,25 @@ void pack_proof(const Circuit& C, const JVal& root, uint64_t* dst, int32_t* rec)
       P.digests(st[s].at("merkle_proof").at("siblings"), base + L.step_path[s], C.step_depth[s], "step siblings");
     }
   }
+}
+
+// ------------------------------------------------------------------ shape variants
+Circuit circuit_shape_variant(const Circuit& base, int num_pis, int final_len) {
+  constexpr int kMaxPis = 1 << 20, kMaxFinal = 1 << 20;   // this build's limits
+  if (num_pis < 0 || num_pis > kMaxPis || final_len < 0 || final_len > kMaxFinal)
+    throw CircuitError("shape variant beyond this build's limits (public inputs / final polynomial length)");
+  Circuit C = base;
+  C.num_pis = num_pis;
+  C.final_len_override = final_len;
+  finalize_circuit(C);   // the same validation; the layout and trace size for these lengths
+  return C;
+}
+
+void proof_shape_json(const JVal& root, int& num_pis, int& final_len) {
+  const size_t np = root.at("public_inputs").arr().size();
+  const size_t nf = root.at("proof").at("opening_proof").at("final_poly").at("coeffs").arr().size();
+  if (np > (size_t)INT32_MAX || nf > (size_t)INT32_MAX) throw ParseError("proof lists too long");
+  num_pis = (int)np; final_len = (int)nf;
 }
 
 // ------------------------------------------------------------------ word-encoded values
@@ -619,6 +640,27 @@ void pack_proof_words(const Circuit& C, const uint64_t* w, size_t n, uint64_t* d
   dst[L.pow] = R.f("pow_witness");
   fields(L.pis, C.num_pis, "public_inputs");   // ProofWithPublicInputs: the_proof, public_inputs
   if (R.i != n) throw ParseError("words: trailing words after ProofWithPublicInputs");
+}
+
+// the final polynomial's and the public inputs' lengths of a word-encoded proof, walking the
+// self-describing list structure of pack_proof_words without assuming the circuit's shapes
+void proof_shape_words(const uint64_t* w, size_t n, int& num_pis, int& final_len) {
+  WordReader R{w, n};
+  R.magic(P2V_WORDS_PROOF_MAGIC);
+  auto skip = [&](int64_t per, const char* what) { const int64_t k = R.len(what); if ((uint64_t)k > (n - R.i) / (uint64_t)per) throw ParseError(std::string("words: bad list length of ") + what); R.i += (size_t)(k * per); return k; };
+  for (int t = 0; t < 3; t++) skip(4, "cap");
+  for (int t = 0; t < 9; t++) skip(2, "openings");
+  for (int64_t s = R.len("commit_phase_merkle_caps"); s > 0; s--) skip(4, "commit cap");
+  for (int64_t q = R.len("query_round_proofs"); q > 0; q--) {
+    for (int64_t t = R.len("evals_proofs"); t > 0; t--) { skip(1, "initial tree leaf"); skip(4, "initial tree siblings"); }
+    for (int64_t s = R.len("steps"); s > 0; s--) { skip(2, "step evals"); skip(4, "step siblings"); }
+  }
+  const int64_t nf = skip(2, "final_poly.coeffs");
+  (void)R.u("pow_witness");
+  const int64_t np = skip(1, "public_inputs");
+  if (R.i != n) throw ParseError("words: trailing words after ProofWithPublicInputs");
+  if (nf > INT32_MAX || np > INT32_MAX) throw ParseError("proof lists too long");
+  final_len = (int)nf; num_pis = (int)np;
 }
 
 // ------------------------------------------------------------------ plonky2 binary proofs

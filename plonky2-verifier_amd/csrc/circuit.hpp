@@ -58,6 +58,7 @@ struct Circuit {
   // VerifierOnlyCircuitData (Types.hs:236-240)
   std::vector<uint64_t> cs_cap;             // 4 words per digest
   uint64_t digest[4] = {0, 0, 0, 0};
+  int final_len_override = -1;               // shape variant (circuit_shape_variant): final_poly length
   // derived
   int cap_len = 0, final_len = 0;
   int oracle_width[4] = {0, 0, 0, 0};       // data columns per initial oracle (Plonk/FRI.hs:56-65)
@@ -105,5 +106,14 @@ struct ProofTemplate {
   bool device_form(std::vector<uint8_t>& skel, std::vector<int32_t>& tok_dst) const;
 };
 GateDesc parse_gate_string(const std::string& s);              // Gate/Parser.hs:107-130
+
+// Shape variants.  The reference reads public_inputs and final_poly.coeffs at whatever length a
+// proof carries (Hash/Sponge.hs:26-31, Plonk/FRI.hs:325-327, Challenge/FRI.hs:83); the packed
+// layout is fixed per circuit, so a proof with other lengths is verified against a variant of the
+// circuit whose layout has them.  Throws CircuitError past this build's limits.
+Circuit circuit_shape_variant(const Circuit& base, int num_pis, int final_len);
+// the two lengths as a proof carries them (JSON / word-encoded); ParseError if they cannot be read
+void proof_shape_json(const JVal& proof, int& num_pis, int& final_len);
+void proof_shape_words(const uint64_t* words, size_t n, int& num_pis, int& final_len);
 
 }  // namespace p2v

@@ -645,7 +645,7 @@ void build_circuit(Circuit& C) {
   j.raw("]},\"quotient_degree_factor\":"); j.i(C.qdf);
   j.raw(",\"num_gate_constraints\":"); j.i(C.num_gate_constraints);
   j.raw(",\"num_constants\":"); j.i(C.num_constants);
-  j.raw(",\"num_public_inputs\":"); j.i(C.num_pis);
+  j.raw(",\"num_public_inputs\":"); j.i(C.num_pis - ((C.ext & 16) ? 1 : 0));   // ext 16: declares one PI fewer than proofs carry
   j.raw(",\"k_is\":"); j.fs(C.k_is.data(), C.k_is.size());
   j.raw(",\"num_partial_products\":"); j.i(C.npp);
   j.raw(",\"num_lookup_polys\":"); j.i(C.nlp);
@@ -1031,6 +1031,7 @@ Witness* make_witness(const Circuit& C, u64 seed) {
 //   1: corrupt the first FRI layer before committing   -> step-0 evaluation mismatch
 //   2: corrupt the last FRI layer (final poly truncated) -> final polynomial mismatch
 //   4: corrupt a quotient opening                        -> Plonk identity fails
+//   8: final polynomial with two trailing zero coefficients (a valid proof of another length)
 std::string make_proof(const Circuit& C, const Witness& W, u64 pi_seed, unsigned flags = 0) {
   Rng rg(pi_seed * 104729 + 5);
   const size_t M = (size_t)1 << C.lde_bits;
@@ -1183,6 +1184,9 @@ std::string make_proof(const Circuit& C, const Witness& W, u64 pi_seed, unsigned
     if (k < final_len) final_poly[k] = ck;
     else if (!(ck.a == 0 && ck.b == 0) && !(flags & 7)) throw std::runtime_error("generator: final polynomial has too high degree");
   }
+  // flags 8: two trailing zero coefficients (the same polynomial at another length: the reference
+  // absorbs and evaluates whatever length it is given, Challenge/FRI.hs:83, Plonk/FRI.hs:325-327)
+  if (flags & 8) { final_poly.push_back(gl::e0()); final_poly.push_back(gl::e0()); }
   d.absorb_e(final_poly);
   // proof of work: find w s.t. the top pow_bits of the squeezed response are zero
   u64 mask = C.pow_bits ? (((1ULL << C.pow_bits) - 1) << (64 - C.pow_bits)) : 0;

@@ -14,11 +14,11 @@ This module keeps that shape:
 and adds the batch form the GPU is built for (verify_proof_batch / BatchVerifier).
 Where the reference raises `error` (failed Merkle proof, folding-step mismatch, unsupported
 circuit) this module raises VerifierError with the same class, and verify_proof returns False
-where the reference returns False, for every proof whose list lengths are the ones the circuit
-implies.  Known divergence: a proof with another number of public inputs or
-final-polynomial coefficients raises P2VError(E_SHAPE) at pack time, where the reference hashes
-/ evaluates whatever it is given and returns False (with overwhelming probability: the
-transcript diverges); any other length mismatch is an `error` in the reference too.
+where the reference returns False.  A proof with another number of public inputs or
+final-polynomial coefficients than the circuit implies is verified, as the reference verifies
+it, against a shape variant of the circuit (p2v_circuit_shape_variant: the packed layout with
+those lengths; the reference hashes / evaluates whatever it is given); any other length
+mismatch is an `error` in the reference too and raises P2VError(E_SHAPE) at pack time.
 
 All verification runs in libp2v's HIP kernels on MI355X; there is no CPU fallback — on a
 machine without a GPU, verification raises P2VError(P2V_E_NODEVICE).
@@ -137,6 +137,9 @@ def lib() -> ctypes.CDLL:
     L.p2v_verify_batch_devices.argtypes = [vp, u64p, sz, i8p, ctypes.POINTER(ctypes.c_int), ctypes.c_int, sz]
     L.p2v_verifier_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
     L.p2v_selftest.argtypes = [ctypes.c_int, ctypes.c_int, u64p, u64p, u64p, sz]
+    L.p2v_proof_shape_json.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    L.p2v_proof_shape_words.argtypes = [u64p, sz, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    L.p2v_circuit_shape_variant.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
     L.p2v_kernel_names.restype = ctypes.c_char_p
     L.p2v_last_error_message.restype = ctypes.c_char_p
     L.p2v_version.restype = ctypes.c_char_p
@@ -211,6 +214,36 @@ class VerifierCircuitData:
     @property
     def handle(self) -> ctypes.c_void_p:
         return self._h
+
+    def shape_variant(self, num_public_inputs: int, final_poly_len: int) -> "VerifierCircuitData":
+        """The same circuit with a packed layout for these public-input / final-polynomial
+        lengths (p2v_circuit_shape_variant); self when they are the circuit's own."""
+        if (num_public_inputs, final_poly_len) == (self.info.num_public_inputs, self.info.final_poly_len):
+            return self
+        cache = self.__dict__.setdefault("_variants", {})
+        key = (num_public_inputs, final_poly_len)
+        if key not in cache:
+            h = ctypes.c_void_p()
+            _check(lib().p2v_circuit_shape_variant(self._h, num_public_inputs, final_poly_len, ctypes.byref(h)))
+            cache[key] = VerifierCircuitData(h.value)
+        return cache[key]
+
+    def for_proof(self, proof_json: Union[str, bytes]) -> "VerifierCircuitData":
+        """The circuit (or its shape variant) whose layout holds this proof's public inputs and
+        final polynomial as given (the reference reads both at any length)."""
+        b = _bytes(proof_json)
+        npi, nf = ctypes.c_int(), ctypes.c_int()
+        if lib().p2v_proof_shape_json(b, len(b), ctypes.byref(npi), ctypes.byref(nf)) != E_OK:
+            return self   # undecodable: packing reports it
+        return self.shape_variant(npi.value, nf.value)
+
+    def for_proof_words(self, words: np.ndarray) -> "VerifierCircuitData":
+        """for_proof for a word-encoded ProofWithPublicInputs (include/p2v.h)."""
+        w = np.ascontiguousarray(words, dtype=np.uint64)
+        npi, nf = ctypes.c_int(), ctypes.c_int()
+        if lib().p2v_proof_shape_words(w.ctypes.data, w.size, ctypes.byref(npi), ctypes.byref(nf)) != E_OK:
+            return self
+        return self.shape_variant(npi.value, nf.value)
 
     def pack_words(self, words: np.ndarray, out: Optional[np.ndarray] = None) -> np.ndarray:
         """A word-encoded ProofWithPublicInputs (include/p2v.h) -> packed u64 words."""
@@ -533,23 +566,33 @@ def device_selftest(op: int, a: np.ndarray, b: Optional[np.ndarray] = None, devi
 
 def verify_proof(vkey: VerifierCircuitData, proof: Union[ProofWithPublicInputs, str, bytes], device: int = 0) -> bool:
     """verifyProof (Plonk/Verifier.hs:56-65): True / False, or VerifierError where the
-    reference raises `error`."""
+    reference raises `error`.  Public inputs and the final polynomial are taken at the length
+    the proof carries (a shape variant of the circuit when it differs, as the reference does)."""
     text = proof.json if isinstance(proof, ProofWithPublicInputs) else _bytes(proof)
-    packed = vkey.pack(text)[None, :]
+    vk = vkey.for_proof(text)
+    packed = vk.pack(text)[None, :]
     res = np.empty(1, dtype=np.int8)
-    _check(lib().p2v_verify_batch(vkey.handle, packed.ctypes.data, 1, res.ctypes.data, device))
+    _check(lib().p2v_verify_batch(vk.handle, packed.ctypes.data, 1, res.ctypes.data, device))
     return _status_to_bool(int(res[0]))
 
 
 def verify_proof_batch(vkey: VerifierCircuitData, proofs: Iterable[Union[ProofWithPublicInputs, str, bytes]],
                        device: int = 0) -> List[Union[bool, VerifierError]]:
-    """Batch form: one entry per proof, True/False or the VerifierError the reference would raise."""
+    """Batch form: one entry per proof, True/False or the VerifierError the reference would raise.
+    Proofs whose public-input / final-polynomial lengths differ from the circuit's are verified in
+    sub-batches of their shape variant."""
     texts = [p.json if isinstance(p, ProofWithPublicInputs) else _bytes(p) for p in proofs]
     if not texts:
         return []
-    packed = vkey.pack_many(texts)
+    groups = {}
+    for i, t in enumerate(texts):
+        groups.setdefault(id(vk := vkey.for_proof(t)), (vk, []))[1].append(i)
     res = np.empty(len(texts), dtype=np.int8)
-    _check(lib().p2v_verify_batch(vkey.handle, packed.ctypes.data, len(texts), res.ctypes.data, device))
+    for vk, idx in groups.values():
+        packed = vk.pack_many([texts[i] for i in idx])
+        sub = np.empty(len(idx), dtype=np.int8)
+        _check(lib().p2v_verify_batch(vk.handle, packed.ctypes.data, len(idx), sub.ctypes.data, device))
+        res[idx] = sub
     out: List[Union[bool, VerifierError]] = []
     for st in res:
         out.append(True if st == ACCEPT else False if st == REJECT else VerifierError(int(st)))

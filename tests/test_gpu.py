@@ -515,6 +515,38 @@ def test_gpu_c3_lookup_batch_full_size(p2v):
             assert np.array_equal(tr[lane], otr), (k, lane)
 
 
+@pytest.mark.parametrize("mode,ext", [(1, 16), (0, 16), (1, 0)])
+def test_gpu_shape_variants_vs_oracle(p2v, mode, ext):
+    """proofs whose public inputs / final polynomial have other lengths than
+    the circuit implies, verified as the reference verifies them (at the proof's own lengths,
+    Hash/Sponge.hs:26-31, Plonk/FRI.hs:325-327) through p2v's shape variants: valid proofs that
+    carry one public input more than the circuit declares (generator ext 16) and a final
+    polynomial with two trailing zero coefficients (flags 8) accept; dropped / added public inputs
+    and final coefficients reject.  verify_proof, verify_proof_batch and the variant's full GPU
+    trace equal the oracle's."""
+    from test_host import _shape_cases
+    O = oracle()
+    gc = gen_circuit(6, 4, 0, 1, 28, 16, 0, mode, ext)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    cases = [("base", gc.proof(1, 1)), ("padded_fp_2", gc.proof(2, 3, flags=8))] + _shape_cases(gc)
+    want = [O.verify_json(gc.common, gc.vkey, pj) for _, pj in cases]
+    if ext & 16:
+        assert want[0] == 1 and want[1] == 1   # the reference accepts them
+    got = p2v.verify_proof_batch(vk, [pj for _, pj in cases])
+    for (name, pj), w, g in zip(cases, want, got):
+        gs = (1 if g is True else 0) if isinstance(g, bool) else g.status
+        assert gs == w, (name, gs, w)
+        if w >= 0:
+            assert p2v.verify_proof(vk, pj) == (w == 1), name
+        else:
+            with pytest.raises(p2v.VerifierError):
+                p2v.verify_proof(vk, pj)
+        v = vk.for_proof(pj)
+        res, tr = p2v.BatchVerifier(v, 0, 1).run(v.pack(pj)[None, :], trace=True)
+        st, otr = O.verify_json(gc.common, gc.vkey, pj, trace=True)
+        assert int(res[0]) == st and np.array_equal(tr[0], otr), name
+
+
 def test_gpu_c5_shard_one_launch(p2v):
     """BASELINE configs[4] (C5), one GPU's shard as the bench runs it: ONE launch of 131 072
     device-resident proofs of the real n = 12 circuit in the 64-proof tiled layout.  Eight

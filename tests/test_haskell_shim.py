@@ -185,6 +185,7 @@ def test_strategy_and_status_encodings(tmp_path):
         assert re.search(rf"\(-{k}\) -> error", hs), k
         assert c[f"e{k}"] == -k
     assert "1    -> True" in hs and "0    -> False" in hs
+    assert re.search(r"^eShape = -(\d+)", hs, re.M).group(1) == "3" and p2v.E_SHAPE == -3   # P2V_E_SHAPE
     assert p2v.ACCEPT == 1 and p2v.REJECT == 0
 
 
@@ -206,6 +207,21 @@ def test_intermediate_trace_offsets_match_the_header():
     assert 4 + 3 * r + 4 * r + 4 + 2 * S + 1 + Q == o["combined"] and o["combined"] + 2 * r == o["quotient"]
     for fn in ("proofChallenges", "evalCombinedPlonkConstraints", "checkCombinedPlonkEquations'"):
         assert re.search(rf"^  , {re.escape(fn)}$", hs, re.M), fn
+
+
+def test_foreign_imports_are_declared_in_the_header():
+    """every C symbol the shim imports is declared in include/p2v.h with the same arity"""
+    hs, hdr = _hs(), open(HDR).read()
+    imports = re.findall(r'foreign import ccall (?:safe|unsafe) "&?(\w+)"\s*\n\s*\w+ :: ([^\n]*)', hs)
+    assert len(imports) >= 14
+    for name, ty in imports:
+        m = re.search(rf"\b{name}\(([^;]*?)\);", hdr, re.S)
+        assert m, name
+        c_args = [a for a in m.group(1).split(",") if a.strip() and a.strip() != "void"]
+        if ty.startswith("FunPtr"):
+            continue
+        hs_args = ty.split("->")[:-1]
+        assert len(hs_args) == len(c_args), (name, hs_args, c_args)
 
 
 if __name__ == "__main__":

@@ -285,3 +285,57 @@ def test_tiled_layout_host_helpers():
         for i in (0, n // 2, n - 1):
             for w in (0, W - 1):
                 assert t[((i // 64) * W + w) * 64 + i % 64] == pm[i, w]
+
+
+def _shape_cases(gc):
+    """(name, proof) pairs whose public-input / final-polynomial lengths differ from the circuit's"""
+    base = gc.proof(1, 1)
+
+    def add_pi(d):
+        d["public_inputs"].append(5)
+
+    def no_pi(d):
+        d["public_inputs"] = []
+
+    def drop_fp(d):
+        d["proof"]["opening_proof"]["final_poly"]["coeffs"].pop()
+
+    def no_fp(d):
+        d["proof"]["opening_proof"]["final_poly"]["coeffs"] = []
+    return [("add_pi", mutate(base, add_pi)), ("no_pi", mutate(base, no_pi)), ("drop_fp", mutate(base, drop_fp)),
+            ("no_fp", mutate(base, no_fp)), ("padded_fp", gc.proof(1, 2, flags=8))]
+
+
+def test_shape_variants_pack_at_the_proofs_lengths():
+    """The reference reads public_inputs and final_poly.coeffs at any length (Hash/Sponge.hs:26-31,
+    Plonk/FRI.hs:325-327): such a proof fails to pack into the circuit's layout (E_SHAPE) and packs
+    into the shape variant for its lengths, JSON and word-encoded alike, with the same values."""
+    p2v = p2v_module()
+    gc = gen_circuit(6, 4, 0, 1, 28, 16, 0, 1)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    assert vk.for_proof(gc.proof(1, 1)) is vk
+    for name, pj in _shape_cases(gc):
+        with pytest.raises(p2v.P2VError) as e:
+            vk.pack(pj)
+        assert e.value.code == p2v.E_SHAPE, name
+        d = json.loads(pj)
+        v = vk.for_proof(pj)
+        assert (v.info.num_public_inputs, v.info.final_poly_len) == (len(d["public_inputs"]),
+                                                                  len(d["proof"]["opening_proof"]["final_poly"]["coeffs"])), name
+        assert v.info.proof_words == vk.info.proof_words + (v.info.num_public_inputs - vk.info.num_public_inputs) + \
+            2 * (v.info.final_poly_len - vk.info.final_poly_len)
+        assert vk.for_proof(pj) is v                               # cached per shape
+        words = p2v.proof_words(pj)
+        assert vk.for_proof_words(words) is v
+        assert np.array_equal(v.pack(pj), v.pack_words(words)), name
+
+
+def test_shape_variant_limits():
+    p2v = p2v_module()
+    gc = gen_circuit(6, 4, 0, 1, 28, 16, 0, 1)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    for npi, nf in ((-1, 4), (4, -1), ((1 << 20) + 1, 4), (4, (1 << 20) + 1)):
+        with pytest.raises(p2v.P2VError) as e:
+            vk.shape_variant(npi, nf)
+        assert e.value.code == p2v.E_SHAPE
+    assert vk.shape_variant(0, 0).info.proof_words == vk.info.proof_words - 4 - 8
