@@ -22,6 +22,7 @@
 extern "C" __global__ void k_transpose(const uint64_t*, int64_t, int, uint64_t*, int);
 extern "C" __global__ void k_phase1(DevCircuit, int, int);
 extern "C" __global__ void k_transcript(DevCircuit, int);
+extern "C" __global__ void k_transcript_x(DevCircuit, int);
 extern "C" __global__ void k_leaf(DevCircuit);
 extern "C" __global__ void k_merkle(DevCircuit);
 extern "C" __global__ void k_fri(DevCircuit);
@@ -93,9 +94,10 @@ struct p2v_verifier {
   int quad_min_batch = 2048;        // auto: quad form from this batch size on
   bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
   int side_prio = 0;                // env P2V_SIDE_PRIO=1: side stream at the device's highest priority (measured: no effect)
-  bool split_phase1 = false;        // env P2V_PHASE1=split: k_transcript (side stream) + k_leaf instead of k_phase1.
+  int split_phase1 = 0;             // env P2V_PHASE1=split (1): k_transcript (side stream) + k_leaf instead of k_phase1.
                                     // Measured (profiles/r02_phase1_split.txt): serial 0.94x, pipelined 1.00x; the
-                                    // transcript waves, latency-bound, stretch to 2.9 ms beside k_leaf
+                                    // transcript waves, latency-bound, stretch to 2.9 ms beside k_leaf.
+                                    // P2V_PHASE1=excl (2): k_transcript_x (main stream, a SIMD per wave) + k_leaf (side)
   bool debug_sync = false;          // env P2V_DEBUG_SYNC=1: name each launch on stderr and synchronise after it (fault isolation)
   // JSON ingest on the device (p2v_verifier_run_json): the current template and its device
   // form, and buffers grown on demand
@@ -337,7 +339,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (const char* ss = getenv("P2V_SINGLE_STREAM")) v->single_stream = ss[0] == '1';
   if (const char* sp = getenv("P2V_SIDE_PRIO")) v->side_prio = sp[0] == '1';
   if (const char* ds = getenv("P2V_DEBUG_SYNC")) v->debug_sync = ds[0] == '1';
-  if (const char* f1 = getenv("P2V_PHASE1")) v->split_phase1 = !strcmp(f1, "split");
+  if (const char* f1 = getenv("P2V_PHASE1")) v->split_phase1 = !strcmp(f1, "split") ? 1 : !strcmp(f1, "excl") ? 2 : 0;
   if (const char* ff = getenv("P2V_FRI_FIRST")) v->fri_first = ff[0] == '1';
   if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : 0;
   DevCircuit& d = v->dc;
@@ -592,6 +594,22 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
       HCK(hipEventRecord(v->dep_p1, st));
       HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));
     }
+  } else if (v->split_phase1 == 2) {
+    // the transcripts first, on st, so their waves claim empty SIMDs before the leaf waves land
+    HCK(hipEventRecord(v->dep_p1, st));   // the batch is ready on st
+    T0(9, st);
+    k_transcript_x<<<nt_blocks, 256, 0, st>>>(d, tl);
+    DBG("k_transcript_x", st);
+    T1(9, st);
+    HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));
+    T0(8, sd);
+    k_leaf<<<(leaf_units + 3) / 4, 256, 0, sd>>>(d);
+    DBG("k_leaf", sd);
+    T1(8, sd);
+    HCK(hipEventRecord(v->dep_tr, sd));
+    HCK(hipStreamWaitEvent(st, v->dep_tr, 0));   // k_merkle reads the leaf digests
+    HCK(hipEventRecord(v->dep_p1, st));          // k_fri / the vanishing kernels read the challenges
+    HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));
   } else {
     HCK(hipEventRecord(v->dep_p1, st));   // the batch is ready on st (H2D, caller's stream order)
     HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));

@@ -105,6 +105,26 @@ __device__ __forceinline__ E row_fold(E h, E ad, bool plus) {   // h_L + alpha^D
   return gl::eadd(h, gl::emul(ad, E{row_up<D>(h.a, plus), row_up<D>(h.b, plus)}));
 }
 
+// sum_m y_{S m + lane} * as^m over the F^2 openings at `off` (n of them), Horner from the top;
+// eight terms' loads are issued ahead of their multiply-adds so the HBM latency overlaps the chain
+template <int S>
+__device__ __forceinline__ E horner_strided(const DevCircuit& c, int64_t off, int64_t n, int lane, int p, E as) {
+  const int64_t M = (n + S - 1) / S;
+  E h = gl::e0();
+  for (int64_t m0 = M - 1; m0 >= 0; m0 -= 8) {
+    E ys[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int64_t i = S * (m0 - u) + lane;
+      ys[u] = (m0 - u >= 0 && i < n) ? lde(c, off + 2 * i, p) : gl::e0();
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (m0 - u >= 0) h = gl::eadd(gl::emul(h, as), ys[u]);
+  }
+  return h;
+}
+
 __device__ __forceinline__ void transcript_row(const DevCircuit& c, int p, const rp::Row& R) {
   const int L = R.L;
   // public inputs hash, Hash/Sponge.hs:26-31 (sponge [] = zero digest)
@@ -171,13 +191,7 @@ __device__ __forceinline__ void transcript_row(const DevCircuit& c, int p, const
 #pragma unroll
   for (int b = 0; b < 2; b++) {
     const int64_t n = b == 0 ? c.n_this : c.n_next, off = b == 0 ? c.o_const : c.o_zs_next;
-    const int64_t M = (n + 15) / 16;
-    E h = gl::e0();
-    for (int64_t m = M - 1; m >= 0; m--) {
-      const int64_t i = 16 * m + L;
-      const E y = i < n ? lde(c, off + 2 * i, p) : gl::e0();
-      h = gl::eadd(gl::emul(h, a16), y);
-    }
+    E h = horner_strided<16>(c, off, n, L, p, a16);
     h = row_fold<1>(h, alpha, R.plus);
     h = row_fold<2>(h, a2, R.plus);
     h = row_fold<4>(h, a4, R.plus);
@@ -219,29 +233,41 @@ __device__ __forceinline__ void transcript_quad(const DevCircuit& c, int p, int 
       if (t == 0) for (int k = 0; k < n; k++) chal(c, a + k, p) = 0;
       continue;
     }
-    const bool ab = type <= TOP_ABSORB_DIGEST;
-    for (int k = 0; k < n; k++) {
-      uint64_t v = 0;
-      if (type == TOP_ABSORB_SOA) v = ld(c, (int64_t)a + k, p);
-      else if (type == TOP_ABSORB_PIH) v = pih[k & 3];
-      else if (type == TOP_ABSORB_DIGEST) v = c.digest[k & 3];
-      bool need;
-      if (ab) { if (!absorbing) { absorbing = true; nbuf = 0; } need = nbuf == 8; }
-      else need = absorbing || outpos < 0;
-      if (need) qp::permute(x, t);   // duplex / re-permute, Challenge/Pure.hs:38-69
-      if (ab) {
-        if (need) nbuf = 0;
-        qp::set_word(x, t, nbuf, v);   // overwrite mode: input lands in the rate part
-        nbuf++;
-      } else {
-        if (need) { absorbing = false; outpos = 7; }
-        uint64_t w = qp::get_word(x, outpos);   // output order state[7], state[6], ... (reverse of take 8)
-        outpos--;
-        if (type == TOP_SQUEEZE_IDX) w &= qmask;
-        if (a + k == CH_FRI_ALPHA(c)) fa0 = w;
-        if (a + k == CH_FRI_ALPHA(c) + 1) fa1 = w;
-        if (t == 0) chal(c, a + k, p) = w;
+    if (type <= TOP_ABSORB_DIGEST) {   // absorb n words, chunk by chunk (lazy duplex, Challenge/Pure.hs:38-69)
+      if (!absorbing) { absorbing = true; nbuf = 0; }
+      for (int k = 0; k < n;) {
+        const int start = nbuf == 8 ? 0 : nbuf;
+        const int take = (8 - start) < (n - k) ? (8 - start) : (n - k);
+        // lane t owns rate positions 3t..3t+2 (qposeidon.h); the chunk's loads are issued
+        // before the permutation so their HBM latency hides under it
+        uint64_t v[3];
+        bool mine[3];
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+          const int pos = 3 * t + j, w = k + pos - start;
+          mine[j] = pos >= start && pos < start + take;
+          v[j] = 0;
+          if (type == TOP_ABSORB_SOA) { if (mine[j]) v[j] = ld(c, (int64_t)a + w, p); }
+          else if (type == TOP_ABSORB_PIH) { const int q = w & 3; v[j] = q == 0 ? pih[0] : q == 1 ? pih[1] : q == 2 ? pih[2] : pih[3]; }
+          else v[j] = c.digest[w & 3];
+        }
+        if (nbuf == 8) { qp::permute(x, t); nbuf = 0; }   // overwrite mode: the rate part is replaced
+#pragma unroll
+        for (int j = 0; j < 3; j++) x[j] = mine[j] ? v[j] : x[j];
+        nbuf += take;
+        k += take;
       }
+      continue;
+    }
+    for (int k = 0; k < n; k++) {   // squeeze
+      const bool need = absorbing || outpos < 0;
+      if (need) { qp::permute(x, t); absorbing = false; outpos = 7; }   // duplex / re-permute, Challenge/Pure.hs:38-69
+      uint64_t w = qp::get_word(x, outpos);   // output order state[7], state[6], ... (reverse of take 8)
+      outpos--;
+      if (type == TOP_SQUEEZE_IDX) w &= qmask;
+      if (a + k == CH_FRI_ALPHA(c)) fa0 = w;
+      if (a + k == CH_FRI_ALPHA(c) + 1) fa1 = w;
+      if (t == 0) chal(c, a + k, p) = w;
     }
   }
   // precomputeReducedOpenings, Plonk/FRI.hs:128-134: Y = sum alpha^i y_i.  Split over the
@@ -252,14 +278,7 @@ __device__ __forceinline__ void transcript_quad(const DevCircuit& c, int p, int 
 #pragma unroll
   for (int b = 0; b < 2; b++) {
     const int64_t n = b == 0 ? c.n_this : c.n_next, off = b == 0 ? c.o_const : c.o_zs_next;
-    const int64_t M = (n + 3) / 4;
-    E h = gl::e0();
-    for (int64_t m = M - 1; m >= 0; m--) {
-      const int64_t i = 4 * m + t;
-      const E y = i < n ? lde(c, off + 2 * i, p) : gl::e0();
-      h = gl::eadd(gl::emul(h, al4), y);
-    }
-    H[b] = h;
+    H[b] = horner_strided<4>(c, off, n, t, p, al4);
   }
 #pragma unroll
   for (int b = 0; b < 2; b++) {
@@ -301,6 +320,20 @@ extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_pe
 // 0.94x): the transcript chains then stretch to the leaf kernel's length; kept for measurement.
 extern "C" __global__ void __launch_bounds__(256) k_transcript(DevCircuit c, int tl) {
   __builtin_amdgcn_s_setprio(3);
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (tl == 16) {
+    rp::Row R;
+    rp::init(R, threadIdx.x);
+    if ((g >> 4) < c.B) transcript_row(c, g >> 4, R);
+  } else {
+    if ((g >> 2) < c.B) transcript_quad(c, g >> 2, g & 3);
+  }
+}
+// k_transcript with SIMDs of its own: the clobbers below make the kernel allocate the whole
+// register file (256 VGPRs + 256 AGPRs), so each transcript wave is alone on its SIMD and issues
+// at the single-wave latency (lat.hip) instead of sharing issue with co-resident leaf waves.
+extern "C" __global__ void __launch_bounds__(256) k_transcript_x(DevCircuit c, int tl) {
+  asm volatile("" ::: "v255", "a255");
   const int g = blockIdx.x * 256 + threadIdx.x;
   if (tl == 16) {
     rp::Row R;
