@@ -125,14 +125,14 @@ __device__ __forceinline__ E horner_strided(const DevCircuit& c, int64_t off, in
   return h;
 }
 
-__device__ __forceinline__ void transcript_row(const DevCircuit& c, int p, const rp::Row& R) {
+__device__ __forceinline__ void transcript_row(const DevCircuit& c, int p, const rp::Row& R, const qp::TLds& T) {
   const int L = R.L;
   // public inputs hash, Hash/Sponge.hs:26-31 (sponge [] = zero digest)
   uint64_t x = 0;
   for (int i = 0; i < c.num_pis; i += 8) {
     const int k = c.num_pis - i;
     if (L < 8 && L < k) x = ld(c, c.pis + i + L, p);
-    x = rp::permute(x, R);
+    x = rp::permute(x, R, T);
   }
   uint64_t pih[4];
 #pragma unroll
@@ -166,7 +166,7 @@ __device__ __forceinline__ void transcript_row(const DevCircuit& c, int p, const
         if (type == TOP_ABSORB_SOA) { if (mine) v = ld(c, (int64_t)a + j, p); }
         else if (type == TOP_ABSORB_PIH) { const int w = j & 3; v = w == 0 ? pih[0] : w == 1 ? pih[1] : w == 2 ? pih[2] : pih[3]; }
         else v = c.digest[j & 3];
-        if (nbuf == 8) { x = rp::permute(x, R); nbuf = 0; }   // overwrite mode: the rate part is replaced
+        if (nbuf == 8) { x = rp::permute(x, R, T); nbuf = 0; }   // overwrite mode: the rate part is replaced
         if (mine) x = v;
         nbuf += take;
         k += take;
@@ -174,7 +174,7 @@ __device__ __forceinline__ void transcript_row(const DevCircuit& c, int p, const
       continue;
     }
     for (int k = 0; k < n; k++) {   // squeeze: output order state[7], state[6], ... (reverse of take 8)
-      if (absorbing || outpos < 0) { x = rp::permute(x, R); absorbing = false; outpos = 7; }
+      if (absorbing || outpos < 0) { x = rp::permute(x, R, T); absorbing = false; outpos = 7; }
       uint64_t w = rp::get_word(x, outpos);
       outpos--;
       if (type == TOP_SQUEEZE_IDX) w &= qmask;
@@ -204,13 +204,13 @@ __device__ __forceinline__ void transcript_row(const DevCircuit& c, int p, const
 // lane).  Higher per-permutation latency than the row form but ~2.3x fewer issue slots in
 // total, which is what matters once the batch is large enough that the transcript hides
 // behind the leaf hashing sharing its launch (the host picks the form, see api.cpp).
-__device__ __forceinline__ void transcript_quad(const DevCircuit& c, int p, int t) {
+__device__ __forceinline__ void transcript_quad(const DevCircuit& c, int p, int t, const qp::TLds& T) {
   // public inputs hash, Hash/Sponge.hs:26-31 (sponge [] = zero digest)
   uint64_t x[3] = {0, 0, 0};
   for (int i = 0; i < c.num_pis; i += 8) {
     const int k = c.num_pis - i;
     for (int j = 0; j < 8 && j < k; j++) qp::set_word(x, t, j, ld(c, c.pis + i + j, p));
-    qp::permute(x, t);
+    qp::permute(x, t, T);
   }
   uint64_t pih[4];
 #pragma unroll
@@ -251,7 +251,7 @@ __device__ __forceinline__ void transcript_quad(const DevCircuit& c, int p, int 
           else if (type == TOP_ABSORB_PIH) { const int q = w & 3; v[j] = q == 0 ? pih[0] : q == 1 ? pih[1] : q == 2 ? pih[2] : pih[3]; }
           else v[j] = c.digest[w & 3];
         }
-        if (nbuf == 8) { qp::permute(x, t); nbuf = 0; }   // overwrite mode: the rate part is replaced
+        if (nbuf == 8) { qp::permute(x, t, T); nbuf = 0; }   // overwrite mode: the rate part is replaced
 #pragma unroll
         for (int j = 0; j < 3; j++) x[j] = mine[j] ? v[j] : x[j];
         nbuf += take;
@@ -261,7 +261,7 @@ __device__ __forceinline__ void transcript_quad(const DevCircuit& c, int p, int 
     }
     for (int k = 0; k < n; k++) {   // squeeze
       const bool need = absorbing || outpos < 0;
-      if (need) { qp::permute(x, t); absorbing = false; outpos = 7; }   // duplex / re-permute, Challenge/Pure.hs:38-69
+      if (need) { qp::permute(x, t, T); absorbing = false; outpos = 7; }   // duplex / re-permute, Challenge/Pure.hs:38-69
       uint64_t w = qp::get_word(x, outpos);   // output order state[7], state[6], ... (reverse of take 8)
       outpos--;
       if (type == TOP_SQUEEZE_IDX) w &= qmask;
@@ -291,22 +291,29 @@ __device__ __forceinline__ void transcript_quad(const DevCircuit& c, int p, int 
   }
 }
 
+// one workgroup of transcripts: `tl` lanes per proof (16: row form, 4: quad form)
+__device__ __forceinline__ void transcript_block(const DevCircuit& c, int tl, const qp::TLds& T) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (tl == 16) {
+    rp::Row R;
+    rp::init(R, threadIdx.x);
+    if ((g >> 4) < c.B) transcript_row(c, g >> 4, R, T);
+  } else {
+    if ((g >> 2) < c.B) transcript_quad(c, g >> 2, g & 3, T);
+  }
+}
+
 // ------------------------------------------------------------------------ phase 1
 // blocks [0, nt_blocks): transcripts, `tl` lanes per proof (16: row form, 4: quad form) at
 // raised wave priority so co-resident leaf waves do not stretch the serial chain; the
 // rest: leaf hashing, 4 units per block.  Transcript blocks come first so they start first.
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_phase1(DevCircuit c, int nt_blocks, int tl) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if ((int)blockIdx.x < nt_blocks) {
+  __shared__ qp::TLds T;
+  if ((int)blockIdx.x < nt_blocks) {   // block-uniform branch: the whole workgroup fills T
     __builtin_amdgcn_s_setprio(3);
-    const int g = blockIdx.x * 256 + threadIdx.x;
-    if (tl == 16) {
-      rp::Row R;
-      rp::init(R, threadIdx.x);
-      if ((g >> 4) < c.B) transcript_row(c, g >> 4, R);
-    } else {
-      if ((g >> 2) < c.B) transcript_quad(c, g >> 2, g & 3);
-    }
+    qp::tlds_fill(T, threadIdx.x, 256);
+    transcript_block(c, tl, T);
     return;
   }
   const int unit = ((int)blockIdx.x - nt_blocks) * 4 + wave;
@@ -320,28 +327,18 @@ extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_pe
 // 0.94x): the transcript chains then stretch to the leaf kernel's length; kept for measurement.
 extern "C" __global__ void __launch_bounds__(256) k_transcript(DevCircuit c, int tl) {
   __builtin_amdgcn_s_setprio(3);
-  const int g = blockIdx.x * 256 + threadIdx.x;
-  if (tl == 16) {
-    rp::Row R;
-    rp::init(R, threadIdx.x);
-    if ((g >> 4) < c.B) transcript_row(c, g >> 4, R);
-  } else {
-    if ((g >> 2) < c.B) transcript_quad(c, g >> 2, g & 3);
-  }
+  __shared__ qp::TLds T;
+  qp::tlds_fill(T, threadIdx.x, 256);
+  transcript_block(c, tl, T);
 }
 // k_transcript with SIMDs of its own: the clobbers below make the kernel allocate the whole
 // register file (256 VGPRs + 256 AGPRs), so each transcript wave is alone on its SIMD and issues
 // at the single-wave latency (lat.hip) instead of sharing issue with co-resident leaf waves.
 extern "C" __global__ void __launch_bounds__(256) k_transcript_x(DevCircuit c, int tl) {
   asm volatile("" ::: "v255", "a255");
-  const int g = blockIdx.x * 256 + threadIdx.x;
-  if (tl == 16) {
-    rp::Row R;
-    rp::init(R, threadIdx.x);
-    if ((g >> 4) < c.B) transcript_row(c, g >> 4, R);
-  } else {
-    if ((g >> 2) < c.B) transcript_quad(c, g >> 2, g & 3);
-  }
+  __shared__ qp::TLds T;
+  qp::tlds_fill(T, threadIdx.x, 256);
+  transcript_block(c, tl, T);
 }
 extern "C" __global__ void __launch_bounds__(256) k_leaf(DevCircuit c) {
   const int unit = (int)blockIdx.x * 4 + (threadIdx.x >> 6);

@@ -41,10 +41,10 @@ __device__ __forceinline__ uint64_t bcast64(uint64_t v, int src) {
 // this lane's round constants (words 3t..3t+2 of round r) as 32-bit halves: they start the
 // MDS row accumulators of round r-1 (the constant addition folded into the previous MDS, as
 // in p2::permute_dev).  In the natural table layout they are contiguous, so each lane does a
-// plain vector load; the caller prefetches one round ahead.
-__device__ __forceinline__ void lane_rc(int r, int t, uint64_t kl[3], uint64_t kh[3]) {
-  const uint64_t* L = p2::c_rc_split.lo + 12 * r + 3 * t;
-  const uint64_t* H = p2::c_rc_split.hi + 12 * r + 3 * t;
+// plain (LDS) load; the caller prefetches one round ahead.
+__device__ __forceinline__ void lane_rc(const p2::RcSplit& rc, int r, int t, uint64_t kl[3], uint64_t kh[3]) {
+  const uint64_t* L = rc.lo + 12 * r + 3 * t;
+  const uint64_t* H = rc.hi + 12 * r + 3 * t;
 #pragma unroll
   for (int k = 0; k < 3; k++) { kl[k] = L[k]; kh[k] = H[k]; }
 }
@@ -116,6 +116,32 @@ __host__ __device__ constexpr QMTab make_qm() {
 #if P2V_PMERGE
 static __constant__ QMTab c_qm = make_qm();
 #endif
+
+// The permutation's per-lane tables, copied into LDS once per transcript workgroup (tlds_fill).
+// A serial chain cannot afford a vector-memory wait inside the permutation: vmcnt retires in
+// issue order, so the first wait on a constant load would also wait for the next chunk's proof
+// loads issued before the permutation (kernels.hip) and expose their HBM latency on the chain.
+// From LDS the tables come back under lgkmcnt, and the proof loads stay in flight throughout.
+struct TLds {
+  p2::RcSplit rc;          // round constants as 32-bit halves, rows 0..30
+  uint64_t rc0[12];        // round 0's constants (added before the first S-box)
+  QBlock qb[p2::PM_NB];    // merged partial-round blocks, per-lane output-row coefficients
+};
+// cooperative copy by the n threads of the workgroup (tid = threadIdx.x); ends with a barrier,
+// so every thread of the workgroup must call it
+__device__ __forceinline__ void tlds_fill(TLds& T, int tid, int n) {
+  const uint64_t* rs = (const uint64_t*)&p2::c_rc_split;
+  uint64_t* rd = (uint64_t*)&T.rc;
+  for (int i = tid; i < (int)(sizeof(p2::RcSplit) / 8); i += n) rd[i] = rs[i];
+  if (tid < 12) T.rc0[tid] = p2::c_round_constants[tid];
+#if P2V_PMERGE
+  const uint64_t* qs = (const uint64_t*)&c_qm;
+  uint64_t* qd = (uint64_t*)T.qb;
+  for (int i = tid; i < (int)(sizeof(QMTab) / 8); i += n) qd[i] = qs[i];
+#endif
+  __syncthreads();
+}
+
 #if P2V_PMERGE && defined(__HIP_DEVICE_COMPILE__)
 #define P2V_QMERGE 1
 
@@ -204,9 +230,9 @@ __device__ __forceinline__ void qblock(uint64_t x[3], int t, const p2::PBlock& B
 // Partial rounds take the S-box off the critical path: the MDS runs on the state with word 0
 // zeroed while lane 0's S-box chain is in flight, then sbox(word 0), broadcast from lane 0,
 // is added with column 0 of M (M[3t+m][0], per lane).
-__device__ __forceinline__ void permute(uint64_t x[3], int t) {
+__device__ __forceinline__ void permute(uint64_t x[3], int t, const TLds& T) {
   {
-    const uint64_t* R = p2::c_round_constants + 3 * t;
+    const uint64_t* R = T.rc0 + 3 * t;
 #pragma unroll
     for (int k = 0; k < 3; k++) x[k] = p2::add_nc(x[k], R[k]);
   }
@@ -217,26 +243,26 @@ __device__ __forceinline__ void permute(uint64_t x[3], int t) {
   uint64_t kl[3], kh[3], nkl[3], nkh[3];
 #if P2V_QMERGE
   // full rounds 0..3, the merged partial-round blocks, full rounds 26..29
-  lane_rc(1, t, nkl, nkh);
+  lane_rc(T.rc, 1, t, nkl, nkh);
 #pragma unroll 1
   for (int r = 0; r < 8; r++) {
     if (r == 4) {
 #if P2V_PMERGE == 4
 #pragma unroll 1
-      for (int b = 0; b < 5; b++) qblock<4>(x, t, p2::c_pm.b[b], c_qm.b[b]);
-      qblock<2>(x, t, p2::c_pm.b[5], c_qm.b[5]);
+      for (int b = 0; b < 5; b++) qblock<4>(x, t, p2::c_pm.b[b], T.qb[b]);
+      qblock<2>(x, t, p2::c_pm.b[5], T.qb[5]);
 #elif P2V_PMERGE == 3
 #pragma unroll 1
-      for (int b = 0; b < 7; b++) qblock<3>(x, t, p2::c_pm.b[b], c_qm.b[b]);
+      for (int b = 0; b < 7; b++) qblock<3>(x, t, p2::c_pm.b[b], T.qb[b]);
 #else
 #pragma unroll 1
-      for (int b = 0; b < 11; b++) qblock<2>(x, t, p2::c_pm.b[b], c_qm.b[b]);
+      for (int b = 0; b < 11; b++) qblock<2>(x, t, p2::c_pm.b[b], T.qb[b]);
 #endif
-      lane_rc(27, t, nkl, nkh);
+      lane_rc(T.rc, 27, t, nkl, nkh);
     }
 #if P2V_PMERGE == 3
     if (r == 4) {   // the schedule's single plain partial round (25)
-      lane_rc(26, t, kl, kh);
+      lane_rc(T.rc, 26, t, kl, kh);
       const uint64_t w0 = x[0];
       x[0] = t == 0 ? 0 : w0;
       uint64_t al[3], ah[3];
@@ -251,7 +277,7 @@ __device__ __forceinline__ void permute(uint64_t x[3], int t) {
     const int rr = r < 4 ? r : r + 22;   // 0..3, 26..29
 #pragma unroll
     for (int k = 0; k < 3; k++) { kl[k] = nkl[k]; kh[k] = nkh[k]; }
-    lane_rc(rr + 2 <= 30 ? rr + 2 : 30, t, nkl, nkh);   // row 30 of the split table is zero
+    lane_rc(T.rc, rr + 2 <= 30 ? rr + 2 : 30, t, nkl, nkh);   // row 30 of the split table is zero
     uint64_t al[3], ah[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) x[k] = p2::sbox_lat(x[k]);
@@ -261,12 +287,12 @@ __device__ __forceinline__ void permute(uint64_t x[3], int t) {
   }
   (void)col0;
 #else
-  lane_rc(1, t, nkl, nkh);
+  lane_rc(T.rc, 1, t, nkl, nkh);
 #pragma unroll 1
   for (int r = 0; r < 30; r++) {
 #pragma unroll
     for (int k = 0; k < 3; k++) { kl[k] = nkl[k]; kh[k] = nkh[k]; }
-    lane_rc(r + 2 <= 30 ? r + 2 : 30, t, nkl, nkh);   // row 30 of the split table is zero
+    lane_rc(T.rc, r + 2 <= 30 ? r + 2 : 30, t, nkl, nkh);   // row 30 of the split table is zero
     uint64_t al[3], ah[3];
     if (r < 4 || r >= 26) {
 #pragma unroll

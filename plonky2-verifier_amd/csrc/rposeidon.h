@@ -105,21 +105,23 @@ __device__ __forceinline__ void conv(const Row& R, uint64_t v, uint64_t& al, uin
 // this lane's round constant (idle lanes read word 11) as 32-bit halves, prefetched one
 // round ahead: it starts the lane's MDS accumulators of the previous round (the constant
 // addition folded into the MDS, as in p2::permute_dev)
-__device__ __forceinline__ void lane_rc(int r, int L, uint64_t& kl, uint64_t& kh) {
+__device__ __forceinline__ void lane_rc(const p2::RcSplit& rc, int r, int L, uint64_t& kl, uint64_t& kh) {
   const int i = 12 * r + (L < 12 ? L : 11);
-  kl = p2::c_rc_split.lo[i];
-  kh = p2::c_rc_split.hi[i];
+  kl = rc.lo[i];
+  kh = rc.hi[i];
 }
 
-// the row's permutation; x = this lane's word (inputs < 2^64, outputs canonical)
-__device__ __forceinline__ uint64_t permute(uint64_t x, const Row& R) {
-  x = p2::add_nc(x, p2::c_round_constants[R.L < 12 ? R.L : 11]);
+// the row's permutation; x = this lane's word (inputs < 2^64, outputs canonical).  T: the
+// constant tables in LDS (qposeidon.h TLds: rc, rc0), for the reason given there
+template <class TT>
+__device__ __forceinline__ uint64_t permute(uint64_t x, const Row& R, const TT& T) {
+  x = p2::add_nc(x, T.rc0[R.L < 12 ? R.L : 11]);
   uint64_t nkl, nkh;
-  lane_rc(1, R.L, nkl, nkh);
+  lane_rc(T.rc, 1, R.L, nkl, nkh);
 #pragma unroll 1
   for (int r = 0; r < 30; r++) {
     uint64_t al = nkl, ah = nkh;
-    lane_rc(r + 2 <= 30 ? r + 2 : 30, R.L, nkl, nkh);   // row 30 of the split table is zero
+    lane_rc(T.rc, r + 2 <= 30 ? r + 2 : 30, R.L, nkl, nkh);   // row 30 of the split table is zero
     if (r < 4 || r >= 26) {
       conv(R, p2::sbox_lat(x), al, ah);
     } else {

@@ -163,10 +163,12 @@ __global__ void __launch_bounds__(256) k_perm(uint64_t* st, int iters, int n) {
 __global__ void __launch_bounds__(256) k_quad_chain(uint64_t* st, int iters, int nq) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   const int q = g >> 2, t = g & 3;
+  __shared__ qp::TLds T;
+  qp::tlds_fill(T, threadIdx.x, blockDim.x);
   if (q >= nq) return;
   uint64_t x[3];
   for (int k = 0; k < 3; k++) x[k] = st[(size_t)(3 * t + k) * nq + q];
-  for (int it = 0; it < iters; it++) qp::permute(x, t);
+  for (int it = 0; it < iters; it++) qp::permute(x, t, T);
   for (int k = 0; k < 3; k++) st[(size_t)(3 * t + k) * nq + q] = x[k];
 }
 
@@ -174,11 +176,13 @@ __global__ void __launch_bounds__(256) k_quad_chain(uint64_t* st, int iters, int
 __global__ void __launch_bounds__(256) k_row_chain(uint64_t* st, int iters, int nr) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   const int q = g >> 4, L = g & 15;
+  __shared__ qp::TLds T;
+  qp::tlds_fill(T, threadIdx.x, blockDim.x);
   if (q >= nr) return;   // whole rows only (nr*16 threads)
   rp::Row R;
   rp::init(R, threadIdx.x);
   uint64_t x = L < 12 ? st[(size_t)L * nr + q] : 0;
-  for (int it = 0; it < iters; it++) x = rp::permute(x, R);
+  for (int it = 0; it < iters; it++) x = rp::permute(x, R, T);
   if (L < 12) st[(size_t)L * nr + q] = x;
 }
 
