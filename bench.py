@@ -53,15 +53,28 @@ VALU_CLOCK_GHZ = 2.4
 VALU_QUAD = 4
 
 
+def pmc_tag():
+    """The latest profile tag (profiles/<tag>_pmc_valu.json AND <tag>_pmc_traffic.json, written
+    together by tools/pmc_summary.py from one tools/profile_round.sh run), so that the line's
+    `valu.issue` and `roofline.traffic` come from the same code version."""
+    import glob
+    tags = []
+    for f in glob.glob(os.path.join(ROOT, "profiles", "*_pmc_valu.json")):
+        tag = os.path.basename(f)[: -len("_pmc_valu.json")]
+        if os.path.exists(os.path.join(ROOT, "profiles", f"{tag}_pmc_traffic.json")):
+            tags.append(tag)
+    return max(tags) if tags else None
+
+
 def valu_roofline(kavg, ms_step, B):
     """VALU issue utilisation from the latest committed rocprofv3 VALU pass
     (profiles/<tag>_pmc_valu.json, same 4096-proof batch): issue cycles per kernel over its
     serial launch time, and for the whole (pipelined) step.  None when no PMC summary exists."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_valu.json")))
-    if not files:
+    tag = pmc_tag()
+    if tag is None:
         return None
-    pm = json.load(open(files[-1]))
+    vfile = os.path.join(ROOT, "profiles", f"{tag}_pmc_valu.json")
+    pm = json.load(open(vfile))
     cyc = {}
     for k, v in pm.items():
         if k.startswith("_") or not v.get("SQ_INSTS_VALU"):
@@ -79,7 +92,7 @@ def valu_roofline(kavg, ms_step, B):
     return {"unit": "G SIMD issue-cycles/s", "peak": peak,
             "step_achieved": round(tot / (ms_step * 1e-3) / 1e9, 1),
             "step_frac": round(tot / (ms_step * 1e-3) / 1e9 / peak, 3),
-            "kernel_frac_serial": per, "source": os.path.relpath(files[-1], ROOT),
+            "kernel_frac_serial": per, "source": os.path.relpath(vfile, ROOT),
             "model": "issue cycles = 4 x (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) per launch; peak = 1024 SIMDs x 2.4 GHz; "
                      "per-instruction costs measured in profiles/r02_valu_rates.txt",
             "note": "all kernels' VALU issue cycles per step over the pipelined step time: the binding resource"}
@@ -573,11 +586,12 @@ def main():
         dom = max(main_stream, key=kavg.get)
         achieved = kb[dom] * B / (kavg[dom] * 1e-3) / 1e9
         # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
-        # (profiles/pmc_traffic.json, corrected per MI355X_MICROARCH.md §HBM), as GB/s over
-        # this run's measured launch time; null if no PMC summary is present.
+        # (profiles/<tag>_pmc_traffic.json, corrected per MI355X_MICROARCH.md §HBM; the same tag
+        # as valu.issue), as GB/s over this run's measured launch time; null if no PMC summary.
         traffic, traffic_bytes = None, None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
+        tag = pmc_tag()
+        pmc = os.path.join(ROOT, "profiles", f"{tag}_pmc_traffic.json") if tag else ""
+        if tag:
             try:
                 traffic_bytes = json.load(open(pmc)).get(dom)
                 if traffic_bytes:
@@ -603,6 +617,7 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
                          "traffic_bytes_per_launch": traffic_bytes, "algorithmic_bytes_per_launch": kb[dom] * B,
+                         "traffic_source": os.path.relpath(pmc, ROOT) if pmc else None,
                          "note": "integer-VALU bound (Poseidon); HBM fraction reported as the metric asks"},
             "valu": {"perms_per_proof": ppp, "perm_rate_G": round(value / world * ppp / 1e9, 3),
                      "issue": valu_roofline(kavg, dt / args.steps * 1e3, B)

@@ -18,6 +18,7 @@
 #define P2V_PROOF_MAJOR 1   // see devcommon.h ld()
 #endif
 #include "gl.h"
+#include "poseidon_constants.h"
 
 extern "C" __global__ void k_transpose(const uint64_t*, int64_t, int, uint64_t*, int);
 extern "C" __global__ void k_phase1(DevCircuit, int, int);
@@ -26,9 +27,19 @@ extern "C" __global__ void k_transcript_x(DevCircuit, int);
 extern "C" __global__ void k_leaf(DevCircuit);
 extern "C" __global__ void k_merkle(DevCircuit);
 extern "C" __global__ void k_fri(DevCircuit);
-extern "C" __global__ void k_vanish(DevCircuit);
-extern "C" __global__ void k_vanish_poseidon(DevCircuit);
-extern "C" __global__ void k_vanish_coset(DevCircuit);
+extern "C" __global__ void k_mtask(DevCircuit);
+extern "C" __global__ void k_mtop(DevCircuit);
+extern "C" __global__ void k_mcheck(DevCircuit);
+extern "C" __global__ void k_mfix(DevCircuit);
+extern "C" __global__ void k_mcap(DevCircuit);
+extern "C" __global__ void k_vanish_r2(DevCircuit);
+extern "C" __global__ void k_vanish_rn(DevCircuit);
+extern "C" __global__ void k_vanish_poseidon_r2(DevCircuit);
+extern "C" __global__ void k_vanish_poseidon_rn(DevCircuit);
+extern "C" __global__ void k_vanish_coset_r2(DevCircuit);
+extern "C" __global__ void k_vanish_coset_rn(DevCircuit);
+extern "C" __global__ void k_vanish_lookup_r2(DevCircuit);
+extern "C" __global__ void k_vanish_lookup_rn(DevCircuit);
 extern "C" __global__ void k_lut(DevCircuit);
 extern "C" __global__ void k_vanish_final(DevCircuit);
 extern "C" __global__ void k_status(DevCircuit, int8_t*, uint64_t*, int64_t);
@@ -45,8 +56,9 @@ int fail(int code, const std::string& msg) { g_err = msg; return code; }
 
 // per-kernel timing slots; k_fri and k_vanish run on the side stream, concurrently with k_merkle
 // (k_leaf + k_transcript: the split form of k_phase1, env P2V_PHASE1=split, measurement only)
-const char* kKernelNames = "k_transpose,k_phase1,k_merkle,k_fri,k_vanish,k_status,k_vanish_final,k_lut,k_leaf,k_transcript";
-constexpr int kNumKernels = 10;
+// (k_mtop: the shared top levels of the Merkle paths, k_mtop + k_mcheck + k_mfix, merkle.hip)
+const char* kKernelNames = "k_transpose,k_phase1,k_merkle,k_fri,k_vanish,k_status,k_vanish_final,k_lut,k_leaf,k_transcript,k_mtop";
+constexpr int kNumKernels = 11;
 
 struct DevBuf {
   void* p = nullptr;
@@ -69,6 +81,33 @@ hipError_t upload(DevBuf& b, const std::vector<T>& h) {
 
 std::mutex g_chain_mu;   // p2v_verifier_chain links (chain_prev / chain_next of every verifier)
 
+// PoseidonGate part 3 (vanish_poseidon.hip): the state entering the fast partial rounds is
+// A'(M sb + rc) (Gate/Custom/Poseidon.hs:92-104: mdsLayer, + fastPartialFirstConstant,
+// mdsInitPartial with A' = diag(1, A), A[i][j] = INITIAL_MATRIX[j][i]); as one affine map of the
+// S-box outputs sb: W = A'M (12 x 12) and k = A' rc, mod p.  Returns [W row-major | k].
+std::vector<uint64_t> poseidon_part3_table() {
+  static const uint64_t init[121] = P2V_FAST_PARTIAL_ROUND_INITIAL_MATRIX_INIT;
+  static const uint64_t rc[12] = P2V_FAST_PARTIAL_FIRST_ROUND_CONSTANT_INIT;
+  static const uint32_t circ[12] = {17, 15, 41, 16, 2, 28, 13, 13, 39, 18, 34, 20};
+  auto M = [&](int i, int j) -> uint64_t { return circ[((j - i) % 12 + 12) % 12] + (i == 0 && j == 0 ? 8 : 0); };
+  auto Ap = [&](int i, int l) -> uint64_t {   // A'[i][l]
+    if (i == 0 || l == 0) return (i == l) ? 1 : 0;
+    return init[11 * (l - 1) + (i - 1)];
+  };
+  std::vector<uint64_t> t(156, 0);
+  for (int i = 0; i < 12; i++) {
+    for (int j = 0; j < 12; j++) {
+      uint64_t acc = 0;
+      for (int l = 0; l < 12; l++) acc = gl::add(acc, gl::mul(Ap(i, l), M(l, j)));
+      t[12 * i + j] = acc;
+    }
+    uint64_t acc = 0;
+    for (int l = 0; l < 12; l++) acc = gl::add(acc, gl::mul(Ap(i, l), rc[l] % gl::P));
+    t[144 + i] = acc;
+  }
+  return t;
+}
+
 }  // namespace
 
 
@@ -79,7 +118,10 @@ struct p2v_verifier {
   DevCircuit dc{};
   std::vector<DevBuf> bufs;
   DevBuf in, soa, chal, leafdig, mk, fbits, qvals, van, vparts, lutre, lutpart, res, trace;
-  DevBuf t_cs, t_kis, t_gkind, t_gpar, t_ggrp, t_gwoff, t_w, t_gs, t_ge, t_lin, t_lout, t_loff, t_llen, t_tw, t_ops, t_vit, t_rin, t_rout, t_roff, t_rch, t_pbase;
+  DevBuf mt_val, mt_cnt, mt_task, mt_fix, mt_flag;   // Merkle top levels (merkle.hip)
+  hipEvent_t dep_mt = nullptr;              // k_mtask done (side stream) -> k_mtop (main)
+  int merkle_trees = 0;                     // trees with k_merkle units (merkle_order prefix)
+  DevBuf t_cs, t_kis, t_gkind, t_gpar, t_ggrp, t_gwoff, t_w, t_gs, t_ge, t_lin, t_lout, t_loff, t_llen, t_tw, t_ops, t_vit, t_rin, t_rout, t_roff, t_rch, t_pbase, t_pw;
   hipEvent_t ev[2 * kNumKernels];   // start/end per kernel
   hipEvent_t dep_p1 = nullptr, dep_side = nullptr, dep_tr = nullptr;
   hipEvent_t p1_done = nullptr;      // recorded on the caller's stream after phase 1 (p2v_verifier_chain)
@@ -300,7 +342,7 @@ void p2v_verifier_free(p2v_verifier* v) {
   }
   (void)hipSetDevice(v->device);
   for (DevBuf* b : {&v->in, &v->soa, &v->chal, &v->leafdig, &v->mk, &v->fbits, &v->qvals, &v->van, &v->vparts, &v->lutre, &v->res, &v->trace, &v->t_cs, &v->t_kis,
-                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit, &v->t_rin, &v->t_rout, &v->t_roff, &v->t_rch, &v->t_pbase, &v->lutpart, &v->j_blob, &v->j_offs, &v->j_skel, &v->j_tok, &v->j_ok,
+                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit, &v->t_rin, &v->t_rout, &v->t_roff, &v->t_rch, &v->t_pbase, &v->t_pw, &v->lutpart, &v->mt_val, &v->mt_cnt, &v->mt_task, &v->mt_fix, &v->mt_flag, &v->j_blob, &v->j_offs, &v->j_skel, &v->j_tok, &v->j_ok,
                     &v->b_rsrc, &v->b_rdst, &v->b_rlen, &v->b_coff, &v->b_cval})
     b->free_();
   if (v->timed) for (auto& e : v->ev) (void)hipEventDestroy(e);
@@ -308,6 +350,7 @@ void p2v_verifier_free(p2v_verifier* v) {
   if (v->dep_side) (void)hipEventDestroy(v->dep_side);
   if (v->dep_tr) (void)hipEventDestroy(v->dep_tr);
   if (v->p1_done) (void)hipEventDestroy(v->p1_done);
+  if (v->dep_mt) (void)hipEventDestroy(v->dep_mt);
   if (v->side) (void)hipStreamDestroy(v->side);
   if (v->h_res) (void)hipHostFree(v->h_res);
   delete v;
@@ -342,6 +385,12 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (const char* f1 = getenv("P2V_PHASE1")) v->split_phase1 = !strcmp(f1, "split") ? 1 : !strcmp(f1, "excl") ? 2 : 0;
   if (const char* ff = getenv("P2V_FRI_FIRST")) v->fri_first = ff[0] == '1';
   if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : 0;
+  // Merkle levels below the cap computed once per distinct node of a proof (merkle.hip); env
+  // P2V_MTOP_K = K > 0 turns it on.  Off by default: measured 1.105 M against 1.129 M proofs/s
+  // pipelined (K = 5; profiles/r03g_merkle_shared.txt): the 11 % fewer compressions do not pay
+  // for the task lists, the gathered loads and the extra launches
+  int mtop_k = 0;
+  if (const char* mk = getenv("P2V_MTOP_K")) mtop_k = atoi(mk);
   DevCircuit& d = v->dc;
   memset(&d, 0, sizeof d);
   d.r = C.r; d.Q = C.num_queries; d.S = (int)C.arities.size(); d.T = 4 + d.S;
@@ -358,12 +407,36 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   d.o_zs = L.o_zs; d.o_pp = L.o_pp; d.o_quot = L.o_quot; d.o_lzs = L.o_lzs; d.o_zs_next = L.o_zs_next; d.o_lzs_next = L.o_lzs_next;
   d.n_this = L.n_this; d.n_next = L.n_next; d.ccaps = L.ccaps; d.final_poly = L.final_poly; d.pow = L.pow; d.q0 = L.q0; d.qstride = L.qstride;
   for (int t = 0; t < 4; t++) { d.leaf[t] = L.leaf[t]; d.path[t] = L.path[t]; }
+  // Merkle top levels: K_t = min(mt_K, depth_t) per tree (a tree whose paths end below the cap
+  // level, depth 0, keeps the whole check in k_merkle); tasks encode q in 8 bits
+  d.mt_K = (mtop_k > 0 && C.num_queries <= 255) ? std::min(mtop_k, 16) : 0;
+  d.mt_L = C.lde_bits - C.cap_height;
+  int& merkle_trees = v->merkle_trees;
+  {
+    int ncls = 0;
+    memset(d.mt_kcls, -1, sizeof d.mt_kcls);
+    for (int t = 0; t < d.T; t++) {
+      const int dep = t < 4 ? C.depth0 : C.step_depth[t - 4];
+      const int K = (d.mt_K > 0 && dep > 0) ? std::min(d.mt_K, dep) : 0;
+      d.mt_k[t] = (int8_t)K;
+      if (K > 0 && d.mt_kcls[K] < 0) { d.mt_kcls[K] = (int8_t)ncls; d.mt_kval[ncls++] = (int8_t)K; }
+    }
+    d.mt_ncls = ncls;
+    d.mt_nbuckets = ncls * (d.mt_K + 1);
+    if (ncls == 0) d.mt_K = 0;
+  }
   {   // unit orders: most expensive tree first (stable), see DevCircuit::leaf_order
     std::vector<std::pair<int64_t, int>> lc, mc;
+    merkle_trees = 0;
     for (int t = 0; t < d.T; t++) {
       const int64_t len = t < 4 ? C.leaf_width[t] : (2ll << C.arities[t - 4]);
       lc.push_back({-(len + 7) / 8, t});
-      mc.push_back({-(int64_t)(t < 4 ? C.depth0 : C.step_depth[t - 4]), t});
+      const int bottom = (t < 4 ? C.depth0 : C.step_depth[t - 4]) - d.mt_k[t];
+      // a tree whose every level is shared (bottom 0, K_t > 0) has no k_merkle units: it sorts
+      // last and the grid stops before it (a depth-0 tree, K_t = 0, keeps its cap check there)
+      const bool none = bottom == 0 && d.mt_k[t] > 0;
+      mc.push_back({none ? 1 : -(int64_t)bottom, t});
+      if (!none) merkle_trees++;
     }
     std::stable_sort(lc.begin(), lc.end()); std::stable_sort(mc.begin(), mc.end());
     for (int k = 0; k < d.T; k++) { d.leaf_order[k] = (int8_t)lc[k].second; d.merkle_order[k] = (int8_t)mc[k].second; }
@@ -453,21 +526,27 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
     for (int g = 0; g < C.n_gate_eval; g++)
       if (gkind[g] == G_POSEIDON) for (int k = 0; k < P2V_POSEIDON_PARTS; k++) item(VI_GATE, g, k, p2v_poseidon_part_first_term(k));
     d.vcls[1] = (int)(vit.size() / 4);
-    for (int g = 0; g < C.n_gate_eval; g++) if (gkind[g] == G_COSET) item(VI_GATE, g, 0, 0);
+    for (int g = 0; g < C.n_gate_eval; g++)   // one item per interpolation chunk (dev.h p2v_coset_parts)
+      if (gkind[g] == G_COSET) {
+        const int64_t parts = p2v_coset_parts((int)gpar[3 * g], gpar[3 * g + 1], gwoff[g + 1] - gwoff[g]);
+        for (int64_t k = 0; k < parts; k++) item(VI_GATE, g, (int)k, p2v_coset_part_first_term(k));
+      }
     d.vcls[2] = (int)(vit.size() / 4);
     for (int g = 0; g < C.n_gate_eval; g++) if (gkind[g] != G_POSEIDON && gkind[g] != G_COSET) item(VI_GATE, g, 0, 0);
     for (int j = 0; j < d.r; j++) item(VI_PP, j, 0, d.r + (int64_t)j * d.n_pp_terms);
+    item(VI_ZS1, 0, 0, 0);
+    d.vcls[3] = (int)(vit.size() / 4);
     if (d.nluts > 0)
       for (int j = 0; j < d.r; j++) item(VI_LOOKUP, j, 0, d.r + (int64_t)d.r * d.n_pp_terms + (int64_t)j * d.n_lookup_terms);
-    item(VI_ZS1, 0, 0, 0);
   }
   d.n_vitems = (int)(vit.size() / 4);
-  d.vcls[3] = d.n_vitems;
+  d.vcls[4] = d.n_vitems;
   hipError_t e = hipSuccess;
 #define UP(buf, vec) if (e == hipSuccess) e = upload(buf, vec)
   UP(v->t_cs, C.cs_cap); UP(v->t_kis, C.k_is); UP(v->t_gkind, gkind); UP(v->t_gpar, gpar); UP(v->t_ggrp, ggrp); UP(v->t_gwoff, gwoff);
   UP(v->t_w, wts); UP(v->t_gs, gs); UP(v->t_ge, ge); UP(v->t_lin, lin); UP(v->t_lout, lout); UP(v->t_loff, loff); UP(v->t_llen, llen); UP(v->t_tw, tw); UP(v->t_ops, ops); UP(v->t_vit, vit);
   UP(v->t_rin, rin); UP(v->t_rout, rout); UP(v->t_roff, roff); UP(v->t_rch, rch); UP(v->t_pbase, pbase);
+  UP(v->t_pw, poseidon_part3_table());
   d.n_lut_pieces = pbase.back();
 #undef UP
   const size_t B = v->Bmax;
@@ -483,6 +562,11 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (e == hipSuccess) e = v->vparts.alloc((size_t)d.n_vitems * 2 * d.r * B * 8);
   if (e == hipSuccess) e = v->lutre.alloc((size_t)d.r * (d.nluts ? d.nluts : 1) * B * 8);
   if (e == hipSuccess) e = v->lutpart.alloc((size_t)d.r * (d.n_lut_pieces ? d.n_lut_pieces : 1) * B * 8);
+  if (e == hipSuccess && d.mt_K > 0) e = v->mt_val.alloc((size_t)d.mt_K * d.Q * d.T * 4 * B * 8);
+  if (e == hipSuccess && d.mt_K > 0) e = v->mt_cnt.alloc((size_t)(d.mt_nbuckets + 1) * 4);
+  if (e == hipSuccess && d.mt_K > 0) e = v->mt_task.alloc((size_t)d.mt_nbuckets * B * d.Q * 4);
+  if (e == hipSuccess && d.mt_K > 0) e = v->mt_fix.alloc((size_t)B * d.T * 4);
+  if (e == hipSuccess && d.mt_K > 0) e = v->mt_flag.alloc((size_t)B * d.T * 4);
   if (e == hipSuccess) e = v->res.alloc(B);
   if (e == hipSuccess) e = hipHostMalloc((void**)&v->h_res, B);
   if (e == hipSuccess) e = v->trace.alloc((size_t)C.trace_words * B * 8);
@@ -491,6 +575,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_side, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_tr, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->p1_done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_mt, hipEventDisableTiming);
   // the side stream carries few, long-latency waves (vanishing items, FRI queries); a
   // high-priority queue for it was measured (P2V_SIDE_PRIO=1) and changed nothing
   if (e == hipSuccess) {
@@ -507,6 +592,8 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   d.lut_in = (const uint64_t*)v->t_lin.p; d.lut_out = (const uint64_t*)v->t_lout.p; d.lut_off = (const int64_t*)v->t_loff.p; d.lut_len = (const int64_t*)v->t_llen.p;
   d.lut_rin = (const uint32_t*)v->t_rin.p; d.lut_rout = (const uint32_t*)v->t_rout.p; d.lut_roff = (const int64_t*)v->t_roff.p; d.lut_rchunks = (const int32_t*)v->t_rch.p; d.lut_pbase = (const int32_t*)v->t_pbase.p;
   d.twiddles = (const uint64_t*)v->t_tw.p; d.tops = (const int32_t*)v->t_ops.p; d.vitems = (const int32_t*)v->t_vit.p;
+  d.pos_w = (const uint64_t*)v->t_pw.p;
+  d.mt_val = (uint64_t*)v->mt_val.p; d.mt_cnt = (int32_t*)v->mt_cnt.p; d.mt_task = (uint32_t*)v->mt_task.p; d.mt_fix = (uint32_t*)v->mt_fix.p; d.mt_flag = (int32_t*)v->mt_flag.p;
   d.soa = (const uint64_t*)v->soa.p; d.chal = (uint64_t*)v->chal.p; d.leafdig = (uint64_t*)v->leafdig.p; d.mk_ok = (uint8_t*)v->mk.p;
   d.fri_bits = (uint32_t*)v->fbits.p; d.qvals = (uint64_t*)v->qvals.p; d.van = (uint64_t*)v->van.p; d.vparts = (uint64_t*)v->vparts.p; d.lutre = (uint64_t*)v->lutre.p; d.lutpart = (uint64_t*)v->lutpart.p;
   *out = v;
@@ -636,18 +723,40 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     DBG("k_fri", sd);
     T1(3, sd);
   }
+  // Merkle top levels: the per-proof task lists first on the side stream (k_mtop waits for them)
+  if (d.mt_K > 0) {
+    HCK(hipMemsetAsync(d.mt_cnt, 0, (size_t)(d.mt_nbuckets + 1) * 4, sd));
+    HCK(hipMemsetAsync(d.mt_flag, 0, (size_t)d.T * d.B * 4, sd));
+    k_mtask<<<(d.Q * NPB + 3) / 4, 256, 0, sd>>>(d);
+    DBG("k_mtask", sd);
+    if (sd != st) HCK(hipEventRecord(v->dep_mt, sd));
+  }
   T0(7, sd);
   if (d.n_lut_pieces > 0) k_lut<<<(d.r * d.n_lut_pieces * NPB + 3) / 4, 256, 0, sd>>>(d);
   DBG("k_lut", sd);
   T1(7, sd);
   // the vanishing items in three kernels (register allocation per class), timed together
   T0(4, sd);
-  if (d.vcls[1] > d.vcls[0]) k_vanish_poseidon<<<((d.vcls[1] - d.vcls[0]) * NPB + 3) / 4, 256, 0, sd>>>(d);
+  // (one wave per work-group; the _r2 forms hold exactly the standard 2 challenge rounds)
+  const bool r2 = d.r == 2;
+  if (d.vcls[1] > d.vcls[0]) {
+    if (r2) k_vanish_poseidon_r2<<<(d.vcls[1] - d.vcls[0]) * NPB, 64, 0, sd>>>(d);
+    else k_vanish_poseidon_rn<<<(d.vcls[1] - d.vcls[0]) * NPB, 64, 0, sd>>>(d);
+  }
   DBG("k_vanish_poseidon", sd);
-  if (d.vcls[2] > d.vcls[1]) k_vanish_coset<<<((d.vcls[2] - d.vcls[1]) * NPB + 3) / 4, 256, 0, sd>>>(d);
+  if (d.vcls[2] > d.vcls[1]) {
+    if (r2) k_vanish_coset_r2<<<(d.vcls[2] - d.vcls[1]) * NPB, 64, 0, sd>>>(d);
+    else k_vanish_coset_rn<<<(d.vcls[2] - d.vcls[1]) * NPB, 64, 0, sd>>>(d);
+  }
   DBG("k_vanish_coset", sd);
-  k_vanish<<<((d.vcls[3] - d.vcls[2]) * NPB + 3) / 4, 256, 0, sd>>>(d);
+  if (r2) k_vanish_r2<<<(d.vcls[3] - d.vcls[2]) * NPB, 64, 0, sd>>>(d);
+  else k_vanish_rn<<<(d.vcls[3] - d.vcls[2]) * NPB, 64, 0, sd>>>(d);
   DBG("k_vanish", sd);
+  if (d.vcls[4] > d.vcls[3]) {
+    if (r2) k_vanish_lookup_r2<<<(d.vcls[4] - d.vcls[3]) * NPB, 64, 0, sd>>>(d);
+    else k_vanish_lookup_rn<<<(d.vcls[4] - d.vcls[3]) * NPB, 64, 0, sd>>>(d);
+  }
+  DBG("k_vanish_lookup", sd);
   T1(4, sd);
   T0(6, sd);
   k_vanish_final<<<(d.B + 255) / 256, 256, 0, sd>>>(d);
@@ -661,9 +770,30 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   }
   if (sd != st) HCK(hipEventRecord(v->dep_side, sd));
   T0(2, st);
-  k_merkle<<<(leaf_units + 3) / 4, 256, 0, st>>>(d);
+  const int merkle_units = d.Q * v->merkle_trees * NPB;
+  if (merkle_units > 0) k_merkle<<<(merkle_units + 3) / 4, 256, 0, st>>>(d);
   DBG("k_merkle", st);
   T1(2, st);
+  if (d.mt_K > 0) {
+    if (sd != st) HCK(hipStreamWaitEvent(st, v->dep_mt, 0));
+    T0(10, st);
+    // one wave per task chunk: the bound per tree is n Q / 64 + K_t (each of its K_t buckets
+    // rounds up once); the waves past the actual chunk count exit at once
+    int64_t chunks = 0;
+    for (int t = 0; t < d.T; t++) if (d.mt_k[t] > 0) chunks += (int64_t)d.n * d.Q / 64 + d.mt_k[t];
+    k_mtop<<<(unsigned)((chunks + 3) / 4), 256, 0, st>>>(d);
+    DBG("k_mtop", st);
+    int top_trees = 0;
+    for (int t = 0; t < d.T; t++) top_trees += d.mt_k[t] > 0;
+    const unsigned top_groups = (unsigned)((top_trees * d.Q * NPB + 3) / 4);
+    k_mcheck<<<top_groups, 256, 0, st>>>(d);
+    DBG("k_mcheck", st);
+    k_mcap<<<top_groups, 256, 0, st>>>(d);
+    DBG("k_mcap", st);
+    k_mfix<<<64, 256, 0, st>>>(d);
+    DBG("k_mfix", st);
+    T1(10, st);
+  }
   if (sd != st) HCK(hipStreamWaitEvent(st, v->dep_side, 0));
   T0(5, st);
   k_status<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(d, dres, dtrace, C.trace_words);

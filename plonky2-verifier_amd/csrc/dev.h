@@ -68,7 +68,20 @@ struct DevCircuit {
   int32_t ntops;
   const int32_t* vitems;           // vanishing work items [n_vitems][4] = {VI_*, a, b, first term}
   int32_t n_vitems;
-  int32_t vcls[4];                 // item ranges of the vanishing kernel classes (Poseidon, coset, rest)
+  int32_t vcls[5];                 // item ranges of the vanishing kernel classes (Poseidon, coset, misc, lookup)
+  // Merkle top levels shared per proof (merkle.hip): mt_K levels below the cap (0: off), the cap's
+  // absolute level mt_L = lde_bits - cap_height, per tree K_t = min(mt_K, depth_t) (0: the whole
+  // path in k_merkle), the distinct K_t values (task classes) and their buffers
+  int32_t mt_K, mt_L, mt_ncls, mt_nbuckets;
+  int8_t mt_k[4 + P2V_MAX_STEPS];
+  int8_t mt_kcls[33];              // K -> class
+  int8_t mt_kval[4 + P2V_MAX_STEPS];   // class -> K
+  uint64_t* mt_val;                // [mt_K][Q][T][4][B]: chain values at levels mt_L - mt_K + 1 ..
+  int32_t* mt_cnt;                 // [mt_nbuckets] task counts, then the count of listed (proof, tree) pairs
+  uint32_t* mt_task;               // [mt_nbuckets][B * Q]: (p << 8) | q
+  uint32_t* mt_fix;                // [B * T]: (p << 8) | t
+  int32_t* mt_flag;                // [T][B]: the (proof, tree) failed an equality check
+  const uint64_t* pos_w;           // PoseidonGate part 3: W = A'M [12][12] then k = A' rc [12] (vanish_poseidon.hip)
   // batch buffers
   const uint64_t* soa;             // [words][B]
   uint64_t* chal;                  // [CH_WORDS][B]
@@ -102,6 +115,28 @@ struct DevCircuit {
 static inline constexpr int p2v_poseidon_part_first_term(int part) {
   return part == 0 ? 0 : part <= 2 ? 17 + 12 * (part - 1) : part == 3 ? 41 : 75 + 12 * (part - 4);
 }
+
+// CosetInterpolationGate (Gate/Custom/CosetInterp.hs:51-121): its chunks start from the witness's
+// intermediate evaluation / product wires, so each chunk is an independent vanishing item (part);
+// the number of chunks the reference evaluates (zipWith worker initials chunks) and the first term
+// of part k in the gate's own numbering (eval_loc: terms 0-1; chunk k < last: 4 terms from 2 + 4k;
+// the last chunk's eval_result term after them)
+#if defined(__HIPCC__)
+#define P2V_HD __host__ __device__
+#else
+#define P2V_HD
+#endif
+static inline P2V_HD int64_t p2v_coset_parts(int bits, int64_t degree, int64_t nweights) {
+  const int64_t npts = (int64_t)1 << bits;
+  const int64_t nint = (npts - 2) / (degree - 1);
+  const int64_t first = degree < npts ? degree : npts;
+  const int64_t nchunks_v = 1 + (npts - first + (degree - 2)) / (degree - 1);
+  const int64_t wfirst = degree < nweights ? degree : nweights;
+  const int64_t nchunks_w = 1 + (nweights - wfirst + (degree - 2)) / (degree - 1);
+  const int64_t nch = nchunks_v < nchunks_w ? nchunks_v : nchunks_w;
+  return nint + 1 < nch ? nint + 1 : nch;
+}
+static inline P2V_HD int64_t p2v_coset_part_first_term(int64_t part) { return part == 0 ? 0 : 2 + 4 * part; }
 
 // challenge buffer offsets (match the P2V_TRACE layout prefix in include/p2v.h)
 #define CH_PI(c) 0

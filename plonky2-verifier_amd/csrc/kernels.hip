@@ -372,7 +372,11 @@ extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCi
     for (int j = 0; j <= s; j++) sh += c.arity[j];
     idx >>= sh; depth = c.step_depth[s]; poff = base + c.step_path[s];
   }
-  const uint64_t* src = c.leafdig + ((int64_t)(q * c.T + t) * 4) * c.B + p;
+  // with the top levels shared per proof (merkle.hip), this kernel stops K_t levels below the
+  // cap and leaves that node in leafdig for k_mtop / k_mcheck
+  const int ktop = c.mt_k[t];
+  uint64_t* src = c.leafdig + ((int64_t)(q * c.T + t) * 4) * c.B + p;
+  if (ktop > 0) depth -= ktop;
   uint64_t cur[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) cur[i] = src[(int64_t)i * c.B];
@@ -390,6 +394,11 @@ extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCi
 #pragma unroll
     for (int i = 0; i < 4; i++) cur[i] = st[i];
     idx >>= 1;
+  }
+  if (ktop > 0) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) src[(int64_t)i * c.B] = cur[i];
+    return;
   }
   // cap_roots !! (idx >> depth)
   bool ok = idx < (uint32_t)c.cap_len;
@@ -453,7 +462,17 @@ __device__ E fold_generic(const DevCircuit& c, int s, int ab, int64_t off, int p
   return gl::escale(c.inv_arity[s], acc);
 }
 
-extern "C" __global__ void __launch_bounds__(256) k_fri(DevCircuit c) {
+// k_fri runs on the side stream beside k_merkle (see vanish.hip P2V_SIDE_WAVES): 5 waves per SIMD
+// caps it at 96 VGPRs, so a wave fits where one k_merkle wave retired (0: compiler default, 122)
+#ifndef P2V_FRI_WAVES
+#define P2V_FRI_WAVES 5
+#endif
+#if P2V_FRI_WAVES > 0
+#define P2V_FRI_ATTR __attribute__((amdgpu_waves_per_eu(P2V_FRI_WAVES)))
+#else
+#define P2V_FRI_ATTR
+#endif
+extern "C" __global__ void __launch_bounds__(256) P2V_FRI_ATTR k_fri(DevCircuit c) {
   const int lane = threadIdx.x & 63;
   const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int NPB = c.B >> 6;

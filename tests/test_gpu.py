@@ -323,6 +323,114 @@ def test_gpu_random_number_mutations_vs_oracle(p2v, nb, mode, lk):
     assert len(set(sts)) >= 3   # the campaign reaches several outcome classes
 
 
+def _merkle_top_cases(gc, base_txt, qidx, info, rnd, n_random=40):
+    """Mutations aimed at the Merkle levels shared per proof (merkle.hip): siblings in the top
+    min(5, depth) levels of representatives and of non-representatives, the same sibling changed
+    identically in two queries on one node, bottom values (leaf evaluations), and random
+    single / double sibling changes in the shared levels."""
+    base = json.loads(base_txt)
+    Q = len(qidx)
+    lt = info.lde_bits - info.cap_height
+
+    def trees():   # (name, shift, depth, sibling-list accessor)
+        out = [(t, 0, info.lde_bits - info.cap_height) for t in range(4)]
+        sh = 0
+        for s, a in enumerate(info.step_arity_bits):
+            sh += a
+            out.append((4 + s, sh, max(0, info.lde_bits - sh - info.cap_height)))
+        return out
+
+    def sibs(d, q, t):
+        qr = d["proof"]["opening_proof"]["query_round_proofs"][q]
+        if t < 4:
+            return qr["initial_trees_proof"]["evals_proofs"][t][1]["siblings"]
+        return qr["steps"][t - 4]["merkle_proof"]["siblings"]
+
+    def bump(d, q, t, l, w=0, by=1):
+        e = sibs(d, q, t)[l]["elements"]
+        e[w] = (e[w] + by) % P
+
+    cases = []
+    for t, sh, dep in trees():
+        K = min(5, dep)
+        for j in range(K):
+            l = dep - K + j
+            A = sh + l + 1
+            groups = {}
+            for q in range(Q):
+                groups.setdefault(qidx[q] >> A, []).append(q)
+            multi = [g for g in groups.values() if len(g) > 1]
+            if not multi:
+                continue
+            g = multi[rnd.randrange(len(multi))]
+            h, q = g[0], g[1 + rnd.randrange(len(g) - 1)]
+            same = (qidx[h] >> (A - 1)) == (qidx[q] >> (A - 1))
+            for who in ((h,), (q,), (h, q)):
+                d = json.loads(base_txt)
+                for x in who:
+                    bump(d, x, t, l, w=j % 4)
+                cases.append(d)
+            if same:   # a different sibling word in each of the two
+                d = json.loads(base_txt)
+                bump(d, h, t, l, 0)
+                bump(d, q, t, l, 1)
+                cases.append(d)
+        if t < 4:   # a bottom value: the leaf of one query of a shared node
+            for q in range(Q):
+                if any(qidx[k] >> (lt - min(5, dep)) == qidx[q] >> (lt - min(5, dep)) for k in range(Q) if k != q):
+                    d = json.loads(base_txt)
+                    ev = d["proof"]["opening_proof"]["query_round_proofs"][q]["initial_trees_proof"]["evals_proofs"][t][0]
+                    ev[0] = (ev[0] + 1) % P
+                    cases.append(d)
+                    break
+    tl = trees()
+    for _ in range(n_random):
+        d = json.loads(base_txt)
+        for _k in range(rnd.randrange(1, 3)):
+            t, sh, dep = tl[rnd.randrange(len(tl))]
+            if dep == 0:
+                continue
+            K = min(5, dep)
+            bump(d, rnd.randrange(Q), t, dep - K + rnd.randrange(K), rnd.randrange(4), rnd.randrange(1, P))
+        cases.append(d)
+    del base
+    return [json.dumps(d, separators=(",", ":")).encode() for d in cases]
+
+
+@pytest.mark.parametrize("nb", [6, 8, 12])
+def test_gpu_merkle_shared_levels_vs_oracle(p2v, nb):
+    """The top Merkle levels computed once per distinct node of a proof (merkle.hip: k_mtask,
+    k_mtop, k_mcheck, k_mfix) against the oracle's per-path verification (Hash/Merkle.hs:27-42):
+    mutations of representatives' and non-representatives' siblings in the shared levels, the
+    same change in two queries on one node, bottom values, random changes.  n = 6: every level of
+    every path is shared (depth 5); n = 8 and 12: k_merkle's bottom levels below them.  Every
+    status and trace word equals the oracle's; the campaign reaches the Merkle failure classes."""
+    import random
+    from support import trace_offsets
+    O = oracle()
+    gc = gen_circuit(nb, 4, 0, 1, 28, 16, 0, 1)
+    base = gc.proof(1, 1)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    info = vk.info
+    st, tr = O.verify_json(gc.common, gc.vkey, base, trace=True)
+    assert st == 1
+    off = trace_offsets(info.num_challenges, info.num_fri_steps, info.num_query_rounds)["query_idx"]
+    qidx = [int(x) for x in tr[off: off + info.num_query_rounds]]
+    cases = [base] + _merkle_top_cases(gc, base, qidx, info, random.Random(nb))
+    # the sharing is opt-in (P2V_MTOP_K, read when a verifier is created); K = 5 and K = 3
+    old = os.environ.get("P2V_MTOP_K")
+    try:
+        for k in ("5", "3"):
+            os.environ["P2V_MTOP_K"] = k
+            sts, _ = _gpu_vs_oracle(p2v, gc, cases)
+    finally:
+        if old is None:
+            os.environ.pop("P2V_MTOP_K", None)
+        else:
+            os.environ["P2V_MTOP_K"] = old
+    assert {-1, -2} <= set(sts), sorted(set(sts))
+
+
 @pytest.mark.parametrize("args,ext", [((6, 4, 0, 1, 28, 16, 0, 1), 0), ((6, 0, 1, 1, 28, 16), 0),
                                       ((6, 4, 0, 1, 28, 16, 0, 1, 7, (3, 2)), 7)])
 def test_gpu_bytes_ingest_matches_host_reader(p2v, args, ext):

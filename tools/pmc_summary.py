@@ -3,7 +3,7 @@
 
 - <tag>_kernel_stats.csv          rocprofv3 --kernel-trace --stats of the default bench command
 - <tag>_kernel_stats_serial.csv   the same with --inflight 1 (averages = bench's kernel_ms)
-- pmc_traffic.json                HBM bytes per launch per kernel from the two PMC passes,
+- <tag>_pmc_traffic.json          HBM bytes per launch per kernel from the two PMC passes,
                                   bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (MI355X_MICROARCH.md
                                   HBM section: gfx950 FETCH_SIZE counts half of wide streaming reads)
 usage: tools/pmc_summary.py <tag> [gpurun_out/prof_<tag>]
@@ -47,7 +47,7 @@ def main():
         f, w = fetch.get(k, 0.0), write.get(k, 0.0)
         out[k] = int(round((2 * f + w) * 1024))
         out[k + "_raw_KiB"] = {"FETCH_SIZE": f, "WRITE_SIZE": w}
-    json.dump(out, open(os.path.join(prof, "pmc_traffic.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(prof, f"{tag}_pmc_traffic.json"), "w"), indent=1)
     vpath = os.path.join(src, "pmc_valu", "run_counter_collection.csv")
     if os.path.exists(vpath):
         valu_summary(vpath, tag, prof)
