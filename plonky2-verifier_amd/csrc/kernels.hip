@@ -354,9 +354,11 @@ extern "C" __global__ void __launch_bounds__(256) k_leaf(DevCircuit c) {
 #else
 #define P2V_MERKLE_ATTR
 #endif
+// (work-groups of 256 threads for large batches, of one wave for small ones, DESIGN.md §7: a few
+// one-wave groups spread over the CUs instead of sharing SIMDs)
 extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCircuit c) {
   const int lane = threadIdx.x & 63;
-  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int unit = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int NPB = c.B >> 6;
   if (unit >= c.Q * c.T * NPB) return;
   const int pb = unit % NPB, qt = unit / NPB;   // (position, query)-major: deepest paths first
@@ -414,6 +416,59 @@ extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCi
     ok = ok && (root == cur[i]);
   }
   c.mk_ok[(int64_t)(q * c.T + t) * c.B + p] = ok ? 1 : 0;
+}
+
+// Latency mode (small batches, api.cpp): the same paths in the row form of the permutation
+// (rposeidon.h: 16 lanes per path, lane L < 12 holding word L), four paths per wave.  A path is a
+// chain of dependent compressions; one lane per path issues at the single-wave latency (~53 us
+// per compression, lat.hip), the row form at ~14 us.  Row = path (tree position, query, proof),
+// proofs fastest; lanes 0..3 hold the path value, lanes 4..7 the other half of the input.
+extern "C" __global__ void __launch_bounds__(256) k_merkle_row(DevCircuit c) {
+  __shared__ qp::TLds T;
+  qp::tlds_fill(T, threadIdx.x, 256);
+  __builtin_amdgcn_s_setprio(3);   // the batch's critical path in this mode
+  rp::Row R;
+  rp::init(R, threadIdx.x);
+  const int L = R.L;
+  const int path = (int)((blockIdx.x * 256 + threadIdx.x) >> 4);
+  const int npaths = c.Q * c.T * c.n;
+  const bool live = path < npaths;   // idle rows still run the permutation (its DPP ops span the row)
+  const int pp = live ? path : 0;
+  const int p = pp % c.n, qt = pp / c.n;
+  const int q = qt % c.Q, t = c.merkle_order[qt / c.Q];
+  const int64_t base = c.q0 + (int64_t)q * c.qstride;
+  uint32_t idx = (uint32_t)chal(c, CH_QIDX(c) + q, p);
+  int depth; int64_t poff;
+  if (t < 4) { depth = c.depth0; poff = base + c.path[t]; }
+  else {
+    const int s = t - 4;
+    int sh = 0;
+    for (int j = 0; j <= s; j++) sh += c.arity[j];
+    idx >>= sh; depth = c.step_depth[s]; poff = base + c.step_path[s];
+  }
+  uint64_t cur = L < 4 ? c.leafdig[((int64_t)(q * c.T + t) * 4 + L) * c.B + p] : 0;
+  for (int l = 0; l < depth; l++) {   // even index: compress(cur, sib), odd: compress(sib, cur)
+    const uint64_t sib = L < 8 ? ld(c, poff + 4 * l + (L & 3), p) : 0;
+    const uint64_t c0 = rp::get_word(cur, 0), c1 = rp::get_word(cur, 1), c2 = rp::get_word(cur, 2), c3 = rp::get_word(cur, 3);
+    const uint64_t cb = L == 4 ? c0 : L == 5 ? c1 : L == 6 ? c2 : c3;
+    const bool odd = idx & 1u;
+    const uint64_t x = L < 4 ? (odd ? sib : cur) : L < 8 ? (odd ? cb : sib) : 0;
+    cur = rp::permute(x, R, T);   // lanes 0..3: the compression's output
+    idx >>= 1;
+  }
+  bool ok = idx < (uint32_t)c.cap_len;
+  const uint32_t ci = ok ? idx : 0;
+  uint64_t root = 0;
+  if (L < 4) {
+    if (t == 0) root = c.cs_cap[ci * 4 + L];
+    else if (t == 1) root = ld(c, c.wcap + ci * 4 + L, p);
+    else if (t == 2) root = ld(c, c.zcap + ci * 4 + L, p);
+    else if (t == 3) root = ld(c, c.qcap + ci * 4 + L, p);
+    else root = ld(c, c.ccaps + (int64_t)(t - 4) * 4 * c.cap_len + ci * 4 + L, p);
+  }
+  const uint64_t eq = (L >= 4 || root == cur) ? 1 : 0;
+  ok = ok && (rp::get_word(eq, 0) & rp::get_word(eq, 1) & rp::get_word(eq, 2) & rp::get_word(eq, 3));
+  if (live && L == 0) c.mk_ok[(int64_t)(q * c.T + t) * c.B + p] = ok ? 1 : 0;
 }
 
 // ------------------------------------------------------------------------ FRI query
@@ -474,7 +529,7 @@ __device__ E fold_generic(const DevCircuit& c, int s, int ab, int64_t off, int p
 #endif
 extern "C" __global__ void __launch_bounds__(256) P2V_FRI_ATTR k_fri(DevCircuit c) {
   const int lane = threadIdx.x & 63;
-  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int unit = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int NPB = c.B >> 6;
   if (unit >= c.Q * NPB) return;
   __builtin_amdgcn_s_setprio(2);   // side stream, concurrent with k_merkle (see k_vanish)

@@ -158,7 +158,9 @@ __device__ __forceinline__ void gate_poseidon(const Vars& V, Acc<R>& A, int part
 }  // namespace
 
 #ifndef P2V_NO_VANISH_KERNELS   // (register experiments include this file for its device code only)
-// one-wave work-groups, at most 112 VGPRs (the space one retiring k_merkle wave leaves)
+// one-wave work-groups at <= 112 VGPRs (the space one retiring k_merkle wave leaves).  (One launch
+// for all three item classes was tried: the fused program stops being inlined, 186 VGPRs and
+// 1.5 KB of scratch per lane; the classes stay separate kernels.)
 extern "C" __global__ void __launch_bounds__(64) k_vanish_poseidon_r2(DevCircuit c) {
   vanish_body<VK_POSEIDON, P2V_R_STD>(c);
 }
