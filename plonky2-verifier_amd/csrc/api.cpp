@@ -139,6 +139,8 @@ struct p2v_verifier {
   int quad_min_batch = 2048;        // auto: quad form from this batch size on
   bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
   int side_prio = 0;                // env P2V_SIDE_PRIO=1: side stream at the device's highest priority (measured: no effect)
+  int side_wg = 256;                // env P2V_SIDE_WG=64: one-wave groups for k_fri / k_vanish_final on the side stream
+                                    // (measured 1.119-1.121 M against 1.128-1.130 M, profiles/r03l_side_wg.txt)
   int split_phase1 = 0;             // env P2V_PHASE1=split (1): k_transcript (side stream) + k_leaf instead of k_phase1.
                                     // Measured (profiles/r02_phase1_split.txt): serial 0.94x, pipelined 1.00x; the
                                     // transcript waves, latency-bound, stretch to 2.9 ms beside k_leaf.
@@ -389,6 +391,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (const char* ds = getenv("P2V_DEBUG_SYNC")) v->debug_sync = ds[0] == '1';
   if (const char* f1 = getenv("P2V_PHASE1")) v->split_phase1 = !strcmp(f1, "split") ? 1 : !strcmp(f1, "excl") ? 2 : 0;
   if (const char* ff = getenv("P2V_FRI_FIRST")) v->fri_first = ff[0] == '1';
+  if (const char* sw = getenv("P2V_SIDE_WG")) v->side_wg = atoi(sw) == 64 ? 64 : 256;
   if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : 0;
   // Merkle levels below the cap computed once per distinct node of a proof (merkle.hip); env
   // P2V_MTOP_K = K > 0 turns it on.  Off by default: measured 1.105 M against 1.129 M proofs/s
@@ -720,13 +723,15 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   }
   HCK(hipEventRecord(v->p1_done, st));   // k_merkle's inputs are complete on st here in both forms
   v->p1_recorded.store(true, std::memory_order_release);
-  // latency mode (at most 128 proofs): the Merkle paths in the row form (k_merkle_row: 16 lanes per
+  // latency mode (at most 64 proofs): the Merkle paths in the row form (k_merkle_row: 16 lanes per
   // path, 4x shorter chains, 16x the lanes), one-wave work-groups for k_fri, and k_fri on a stream
   // of its own beside the vanishing kernels instead of after them.  Measured:
-  // one proof 2.19 -> 1.98 ms; from 256 proofs on the row form's lanes cost more than its latency saves
-  const bool lat = d.n <= 128;
+  // one proof 2.19 -> 1.98 ms, 64 proofs 2.18 -> 2.10 ms; at 128 proofs the row form's lanes cost more than its latency saves
+  const bool lat = d.n <= 64;
   const int mk_wg = lat ? 64 : 256;
   const bool fri2 = lat && sd != st;
+  // side-stream work-groups of k_fri / k_vanish_final (P2V_SIDE_WG, measurement)
+  const int side_wg = v->side_wg;
   if (fri2) {
     HCK(hipStreamWaitEvent(v->side2, v->p1_done, 0));
     T0(3, v->side2);
@@ -741,7 +746,7 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   // (longest waves, most registers) are what remains when k_merkle's waves retire
   if (v->fri_first && !fri2) {
     T0(3, sd);
-    k_fri<<<(d.Q * NPB + 3) / 4, 256, 0, sd>>>(d);
+    k_fri<<<(d.Q * NPB * 64 + side_wg - 1) / side_wg, side_wg, 0, sd>>>(d);
     DBG("k_fri", sd);
     T1(3, sd);
   }
@@ -781,12 +786,12 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   DBG("k_vanish_lookup", sd);
   T1(4, sd);
   T0(6, sd);
-  k_vanish_final<<<(d.B + 255) / 256, 256, 0, sd>>>(d);
+  k_vanish_final<<<(d.B + side_wg - 1) / side_wg, side_wg, 0, sd>>>(d);
   DBG("k_vanish_final", sd);
   T1(6, sd);
   if (!v->fri_first && !fri2) {
     T0(3, sd);
-    k_fri<<<(d.Q * NPB + 3) / 4, 256, 0, sd>>>(d);
+    k_fri<<<(d.Q * NPB * 64 + side_wg - 1) / side_wg, side_wg, 0, sd>>>(d);
     DBG("k_fri", sd);
     T1(3, sd);
   }

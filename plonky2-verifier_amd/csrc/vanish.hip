@@ -42,8 +42,9 @@ extern "C" __global__ void __launch_bounds__(64) k_vanish_lookup_r2(DevCircuit c
 extern "C" __global__ void __launch_bounds__(64) k_vanish_lookup_rn(DevCircuit c) { vanish_body<VK_LOOKUP, P2V_MAX_R>(c); }
 
 // sum of the item partials, then Q(zeta)(zeta^n - 1) == C(zeta), Plonk/Verifier.hs:35-51
+// (one-wave work-groups, like the other side-stream kernels: a wave fits where one k_merkle wave retired)
 extern "C" __global__ void __launch_bounds__(256) k_vanish_final(DevCircuit c) {
-  const int p = blockIdx.x * 256 + threadIdx.x;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= c.B) return;
   const int r = c.r;
   const E one = gl::eb(1);
