@@ -451,6 +451,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=2, help="batches in flight per GPU (workspaces/streams)")
     ap.add_argument("--stagger", type=int, default=0, choices=(0, 1),
                     help="1: chain the in-flight workspaces (p2v_verifier_chain) so their phase 1 alternate")
+    ap.add_argument("--lookahead", type=int, default=0, choices=(0, 1),
+                    help="1: P2V_FLAG_LOOKAHEAD (each batch's transcript on its own stream, ahead of the workspace's earlier batches)")
     ap.add_argument("--layout", choices=("tiled", "proof-major"), default="tiled",
                     help="device-resident batch layout: 64-proof tiles (P2V_FLAG_INPUT_TILED, coalesced loads) or proof-major rows")
     ap.add_argument("--ext", type=int, default=0, help="P2V_EXT_* flags of the workload circuit (1 MinSize arities, 2 hiding, 4 hash_or_noop)")
@@ -546,7 +548,7 @@ def main():
         for i in range(k):
             j = i % nv if pipelined else 0
             bvs[j].run_device(d_proofs.data_ptr(), B, d_res[j].data_ptr(), stream=streams[j].cuda_stream, sync=not pipelined,
-                              tiled=lay_tiled)
+                              tiled=lay_tiled, lookahead=bool(args.lookahead))
             if not pipelined:
                 for name, v in bvs[0].last_timings().items():
                     ktimes.setdefault(name, []).append(v)
@@ -558,7 +560,7 @@ def main():
 
     for i in range(args.warmup):
         bvs[i % nv].run_device(d_proofs.data_ptr(), B, d_res[i % nv].data_ptr(), stream=streams[i % nv].cuda_stream, sync=False,
-                               tiled=lay_tiled)
+                               tiled=lay_tiled, lookahead=bool(args.lookahead))
     torch.cuda.synchronize(dev)
     assert all(bool((r == d_expect).all()) for r in d_res[:max(1, min(nv, args.warmup))]), "batch statuses differ from the expected ones"
     # serial pass: per-kernel durations (HIP events recorded on the run's streams inside libp2v)
@@ -611,7 +613,7 @@ def main():
                                    f"{' in 64-proof tiles' if lay_tiled else ' proof-major'}",
                        "global_batch": B * world, "degree_bits": info.degree_bits, "parallelism": f"proof-sharded x{world}",
                        **({"ext": args.ext} if args.ext else {}),
-                       "inflight": nv, "stagger": bool(args.stagger and nv > 1)},
+                       "inflight": nv, "stagger": bool(args.stagger and nv > 1), "lookahead": bool(args.lookahead)},
             "serial": {"value": round(total / dt_serial, 1), "ms_per_step": round(dt_serial / args.steps * 1e3, 4),
                        "note": "one batch at a time, host-synchronised per step; kernel_ms and roofline come from this pass"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",

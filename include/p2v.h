@@ -204,6 +204,11 @@ int  p2v_circuit_shape_variant(const p2v_circuit* c, int num_public_inputs, int 
 #define P2V_FLAG_NO_SYNC       4u  /* do not synchronise the stream before returning          */
 #define P2V_FLAG_INPUT_TILED  16u  /* `proofs` is in the 64-proof tiled layout below (p2v_tile_proofs) instead of
                                       proof-major: every wave's loads are then whole 512-B rows          */
+#define P2V_FLAG_LOOKAHEAD    32u  /* with P2V_FLAG_INPUT_DEVICE: the batch is complete in device memory when the
+                                       call is made (nothing queued on `stream` still writes it), so its transcript
+                                       may run ahead of this workspace's earlier batches, on a stream of its own
+                                       with a second challenge buffer, overlapping their Merkle / FRI work
+                                       (DESIGN.md §5.2); results are unchanged                                  */
 #define P2V_FLAG_UNIT_FILTERS  8u  /* parity mode: every gate filter and lookup selector := 1, so the
                                       trace's combined values C_i expose every constraint program
                                       (the oracle's or_verify full_trace bit 1); statuses are then

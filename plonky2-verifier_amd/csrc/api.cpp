@@ -132,6 +132,13 @@ struct p2v_verifier {
   hipStream_t side = nullptr;
   hipStream_t side2 = nullptr;      // small batches: k_fri beside the vanishing kernels (latency mode)
   hipEvent_t dep_fri = nullptr;
+  // transcript lookahead (P2V_FLAG_LOOKAHEAD): its own stream, two challenge buffers used by
+  // alternate runs; tr_done[s]: the transcript into buffer s is complete, chal_free[s]: the run
+  // that read buffer s has completed (k_status)
+  hipStream_t ts = nullptr;
+  hipEvent_t tr_done[2] = {nullptr, nullptr}, chal_free[2] = {nullptr, nullptr};
+  DevBuf chal2;
+  unsigned la_seq = 0;
   float last_ms[kNumKernels] = {0};
   bool timed = false;
   bool fri_first = false;           // side stream order: k_fri before the vanishing kernels (env P2V_FRI_FIRST=1)
@@ -347,7 +354,7 @@ void p2v_verifier_free(p2v_verifier* v) {
   }
   (void)hipSetDevice(v->device);
   for (DevBuf* b : {&v->in, &v->soa, &v->chal, &v->leafdig, &v->mk, &v->fbits, &v->qvals, &v->van, &v->vparts, &v->lutre, &v->res, &v->trace, &v->t_cs, &v->t_kis,
-                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit, &v->t_rin, &v->t_rout, &v->t_roff, &v->t_rch, &v->t_pbase, &v->t_pw, &v->lutpart, &v->mt_val, &v->mt_cnt, &v->mt_task, &v->mt_fix, &v->mt_flag, &v->j_blob, &v->j_offs, &v->j_skel, &v->j_tok, &v->j_ok,
+                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit, &v->t_rin, &v->t_rout, &v->t_roff, &v->t_rch, &v->t_pbase, &v->t_pw, &v->lutpart, &v->mt_val, &v->mt_cnt, &v->mt_task, &v->mt_fix, &v->mt_flag, &v->chal2, &v->j_blob, &v->j_offs, &v->j_skel, &v->j_tok, &v->j_ok,
                     &v->b_rsrc, &v->b_rdst, &v->b_rlen, &v->b_coff, &v->b_cval})
     b->free_();
   if (v->timed) for (auto& e : v->ev) (void)hipEventDestroy(e);
@@ -358,6 +365,11 @@ void p2v_verifier_free(p2v_verifier* v) {
   if (v->dep_mt) (void)hipEventDestroy(v->dep_mt);
   if (v->side) (void)hipStreamDestroy(v->side);
   if (v->side2) (void)hipStreamDestroy(v->side2);
+  if (v->ts) (void)hipStreamDestroy(v->ts);
+  for (int k = 0; k < 2; k++) {
+    if (v->tr_done[k]) (void)hipEventDestroy(v->tr_done[k]);
+    if (v->chal_free[k]) (void)hipEventDestroy(v->chal_free[k]);
+  }
   if (v->dep_fri) (void)hipEventDestroy(v->dep_fri);
   if (v->h_res) (void)hipHostFree(v->h_res);
   delete v;
@@ -562,6 +574,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (e == hipSuccess) e = v->in.alloc((size_t)L.words * v->Bmax * 8);   // whole 64-proof tiles (P2V_FLAG_INPUT_TILED)
   if (e == hipSuccess && !P2V_PROOF_MAJOR) e = v->soa.alloc((size_t)L.words * B * 8);   // the transposed batch
   if (e == hipSuccess) e = v->chal.alloc(chw * B * 8);
+  if (e == hipSuccess) e = v->chal2.alloc(chw * B * 8);
   if (e == hipSuccess) e = v->leafdig.alloc((size_t)d.Q * d.T * 4 * B * 8);
   if (e == hipSuccess) e = v->mk.alloc((size_t)d.Q * d.T * B);
   if (e == hipSuccess) e = v->fbits.alloc((size_t)d.Q * B * 4);
@@ -593,7 +606,13 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
     else
       e = hipStreamCreateWithFlags(&v->side, hipStreamNonBlocking);
   }
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&v->side2, hipStreamNonBlocking);
+  // (the latency-mode and lookahead streams are created on first use: every stream a process
+  // creates may take one of its few hardware queues, GPU_MAX_HW_QUEUES = 4, and two workspaces'
+  // main and side streams must not share one)
+  for (int k = 0; k < 2 && e == hipSuccess; k++) {
+    e = hipEventCreateWithFlags(&v->tr_done[k], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&v->chal_free[k], hipEventDisableTiming);
+  }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_fri, hipEventDisableTiming);
   if (e != hipSuccess) { p2v_verifier_free(v); return fail(P2V_E_DEVICE, std::string("device allocation: ") + hipGetErrorString(e)); }
   d.cs_cap = (const uint64_t*)v->t_cs.p; d.k_is = (const uint64_t*)v->t_kis.p; d.gate_kind = (const int32_t*)v->t_gkind.p;
@@ -682,7 +701,28 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     if (v->chain_prev && v->chain_prev->p1_recorded.load(std::memory_order_acquire))
       HCK(hipStreamWaitEvent(st, v->chain_prev->p1_done, 0));
   }
-  if (!v->split_phase1 || sd == st) {
+  // transcript lookahead: the transcript on v->ts into the challenge buffer of this run's parity,
+  // after the run that last read that buffer; the leaf hashing on st; k_merkle after both
+  const bool la = (flags & P2V_FLAG_LOOKAHEAD) && (flags & P2V_FLAG_INPUT_DEVICE) && sd != st && !v->chain_prev;
+  int la_slot = 0;
+  if (la) {
+    if (!v->ts) HCK(hipStreamCreateWithFlags(&v->ts, hipStreamNonBlocking));
+    la_slot = (int)(v->la_seq++ & 1u);
+    d.chal = (uint64_t*)(la_slot ? v->chal2.p : v->chal.p);
+    HCK(hipStreamWaitEvent(v->ts, v->chal_free[la_slot], 0));
+    T0(9, v->ts);
+    k_transcript<<<nt_blocks, 256, 0, v->ts>>>(d, tl);
+    DBG("k_transcript", v->ts);
+    T1(9, v->ts);
+    HCK(hipEventRecord(v->tr_done[la_slot], v->ts));
+    T0(8, st);
+    k_leaf<<<(leaf_units + 3) / 4, 256, 0, st>>>(d);
+    DBG("k_leaf", st);
+    T1(8, st);
+    HCK(hipStreamWaitEvent(st, v->tr_done[la_slot], 0));   // k_merkle reads the query indices
+    HCK(hipEventRecord(v->dep_p1, st));                     // the side kernels read the challenges
+    HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));
+  } else if (!v->split_phase1 || sd == st) {
     T0(1, st);
     k_phase1<<<nt_blocks + (leaf_units + 3) / 4, 256, 0, st>>>(d, nt_blocks, tl);
     DBG("k_phase1", st);
@@ -730,6 +770,7 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   const bool lat = d.n <= 64;
   const int mk_wg = lat ? 64 : 256;
   const bool fri2 = lat && sd != st;
+  if (fri2 && !v->side2) HCK(hipStreamCreateWithFlags(&v->side2, hipStreamNonBlocking));
   // side-stream work-groups of k_fri / k_vanish_final (P2V_SIDE_WG, measurement)
   const int side_wg = v->side_wg;
   if (fri2) {
@@ -828,6 +869,10 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   k_status<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(d, dres, dtrace, C.trace_words);
   DBG("k_status", st);
   T1(5, st);
+  // the challenge buffer's last reader is done (a run without the flag used buffer 0: a later
+  // lookahead transcript into buffer 0 must wait for it as well)
+  if (la) HCK(hipEventRecord(v->chal_free[la_slot], st));
+  else if (sd != st) HCK(hipEventRecord(v->chal_free[0], st));
 #undef T0
 #undef T1
 #undef DBG

@@ -66,6 +66,7 @@ FLAG_RESULT_DEVICE = 2
 FLAG_NO_SYNC = 4
 FLAG_UNIT_FILTERS = 8   # parity mode (tests only): every gate filter / lookup selector := 1
 FLAG_INPUT_TILED = 16   # the batch in 64-proof tiles [n/64][words][64] (tile_proofs)
+FLAG_LOOKAHEAD = 32     # the device batch is complete at the call: its transcript may run ahead (include/p2v.h)
 
 
 class P2VError(RuntimeError):
@@ -412,11 +413,14 @@ class BatchVerifier:
         return words, codes
 
     def run_device(self, proofs_ptr: int, n: int, results_ptr: int, stream: int = 0, trace_ptr: int = 0,
-                   sync: bool = True, tiled: bool = False) -> None:
+                   sync: bool = True, tiled: bool = False, lookahead: bool = False) -> None:
         """Device-resident batch: raw device pointers (e.g. torch tensor .data_ptr()) and a
         hipStream_t handle (torch.cuda.current_stream().cuda_stream).  tiled: the batch is in the
-        64-proof tiled layout (P2V_FLAG_INPUT_TILED, tile_proofs)."""
-        flags = FLAG_INPUT_DEVICE | FLAG_RESULT_DEVICE | (0 if sync else FLAG_NO_SYNC) | (FLAG_INPUT_TILED if tiled else 0)
+        64-proof tiled layout (P2V_FLAG_INPUT_TILED, tile_proofs).  lookahead: the batch is already
+        complete in device memory, so its transcript may run ahead of this workspace's earlier
+        batches (P2V_FLAG_LOOKAHEAD)."""
+        flags = (FLAG_INPUT_DEVICE | FLAG_RESULT_DEVICE | (0 if sync else FLAG_NO_SYNC) | (FLAG_INPUT_TILED if tiled else 0)
+                 | (FLAG_LOOKAHEAD if lookahead else 0))
         _check(lib().p2v_verifier_run(self._h, ctypes.c_void_p(proofs_ptr), n, ctypes.c_void_p(results_ptr),
                                       ctypes.c_void_p(trace_ptr) if trace_ptr else None, ctypes.c_void_p(stream), flags))
 

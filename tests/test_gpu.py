@@ -286,6 +286,37 @@ def test_gpu_chained_workspaces(p2v):
     assert np.array_equal(bvs[1].run(batches[3]), want[3])
 
 
+@pytest.mark.parametrize("B,tiled", [(200, False), (2048, True)])
+def test_gpu_transcript_lookahead(p2v, B, tiled):
+    """P2V_FLAG_LOOKAHEAD: each batch's transcript runs on the workspace's own transcript stream
+    into one of two challenge buffers, ahead of the workspace's earlier batches.  Two workspaces,
+    12 different batches (rotations of a pool with valid and corrupted proofs) in flight without
+    host syncs, each workspace reused every other batch (both challenge buffers cycle): every
+    batch's statuses equal a plain synchronous run's.  B = 2048 runs the quad transcript and the
+    tiled layout, B = 200 the row transcript."""
+    import torch
+    gc = gen_circuit(6, 4, 0, 1, 28, 16, 0, 1)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    pool = [gc.proof(1, 1), gc.proof(2, 2), gc.proof(1, 3, flags=1), gc.proof(1, 4, flags=4), gc.proof(2, 5, flags=2)]
+    packed = vk.pack_many(pool)
+    nb = 12
+    batches = [np.ascontiguousarray(packed[(np.arange(B) * (k + 1) + k) % len(pool)]) for k in range(nb)]
+    ref = p2v.BatchVerifier(vk, 0, B)
+    want = [ref.run(b) for b in batches]
+    bvs = [p2v.BatchVerifier(vk, 0, B) for _ in range(2)]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    d_in = [torch.from_numpy((p2v.tile_proofs(b) if tiled else b).view(np.int64)).cuda() for b in batches]
+    d_res = [torch.full((B,), 7, dtype=torch.int8, device="cuda") for _ in batches]
+    torch.cuda.synchronize()
+    for k in range(nb):
+        bvs[k % 2].run_device(d_in[k].data_ptr(), B, d_res[k].data_ptr(), stream=streams[k % 2].cuda_stream, sync=False,
+                              tiled=tiled, lookahead=True)
+    torch.cuda.synchronize()
+    for k in range(nb):
+        assert np.array_equal(d_res[k].cpu().numpy(), want[k]), k
+    assert {1, -3, 0} <= set(np.concatenate(want).tolist())
+
+
 def _number_paths(d, path=()):
     """Every number leaf of a JSON value, as a key path."""
     if isinstance(d, dict):
