@@ -27,6 +27,7 @@ extern "C" __global__ void k_transcript_x(DevCircuit, int);
 extern "C" __global__ void k_leaf(DevCircuit);
 extern "C" __global__ void k_merkle(DevCircuit);
 extern "C" __global__ void k_merkle_row(DevCircuit);
+extern "C" __global__ void k_merkle_bottom(DevCircuit);
 extern "C" __global__ void k_fri(DevCircuit);
 extern "C" __global__ void k_mtask(DevCircuit);
 extern "C" __global__ void k_mtop(DevCircuit);
@@ -840,7 +841,8 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   T0(2, st);
   const int merkle_units = d.Q * v->merkle_trees * NPB;
   if (lat && d.mt_K == 0) k_merkle_row<<<(unsigned)(((int64_t)d.Q * d.T * d.n * 16 + 255) / 256), 256, 0, st>>>(d);
-  else if (merkle_units > 0) k_merkle<<<(merkle_units * 64 + mk_wg - 1) / mk_wg, mk_wg, 0, st>>>(d);
+  else if (merkle_units > 0 && d.mt_K > 0) k_merkle_bottom<<<(merkle_units + 3) / 4, 256, 0, st>>>(d);
+  else if (merkle_units > 0) k_merkle<<<(merkle_units + 3) / 4, 256, 0, st>>>(d);
   DBG("k_merkle", st);
   T1(2, st);
   if (d.mt_K > 0) {

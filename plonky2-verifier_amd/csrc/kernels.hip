@@ -354,11 +354,13 @@ extern "C" __global__ void __launch_bounds__(256) k_leaf(DevCircuit c) {
 #else
 #define P2V_MERKLE_ATTR
 #endif
-// (work-groups of 256 threads for large batches, of one wave for small ones, DESIGN.md §7: a few
-// one-wave groups spread over the CUs instead of sharing SIMDs)
-extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCircuit c) {
+// BOTTOM: with the top levels shared per proof (merkle.hip, opt-in), the paths stop K_t levels
+// below the cap and leave that node in leafdig for k_mtop / k_mcheck (a kernel of its own, so
+// that the default k_merkle keeps its 77 VGPRs and no scratch)
+template <bool BOTTOM>
+__device__ __forceinline__ void merkle_unit(const DevCircuit& c) {
   const int lane = threadIdx.x & 63;
-  const int unit = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int NPB = c.B >> 6;
   if (unit >= c.Q * c.T * NPB) return;
   const int pb = unit % NPB, qt = unit / NPB;   // (position, query)-major: deepest paths first
@@ -374,11 +376,8 @@ extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCi
     for (int j = 0; j <= s; j++) sh += c.arity[j];
     idx >>= sh; depth = c.step_depth[s]; poff = base + c.step_path[s];
   }
-  // with the top levels shared per proof (merkle.hip), this kernel stops K_t levels below the
-  // cap and leaves that node in leafdig for k_mtop / k_mcheck
-  const int ktop = c.mt_k[t];
   uint64_t* src = c.leafdig + ((int64_t)(q * c.T + t) * 4) * c.B + p;
-  if (ktop > 0) depth -= ktop;
+  if constexpr (BOTTOM) depth -= c.mt_k[t];
   uint64_t cur[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) cur[i] = src[(int64_t)i * c.B];
@@ -397,7 +396,7 @@ extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCi
     for (int i = 0; i < 4; i++) cur[i] = st[i];
     idx >>= 1;
   }
-  if (ktop > 0) {
+  if constexpr (BOTTOM) {
 #pragma unroll
     for (int i = 0; i < 4; i++) src[(int64_t)i * c.B] = cur[i];
     return;
@@ -417,6 +416,8 @@ extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCi
   }
   c.mk_ok[(int64_t)(q * c.T + t) * c.B + p] = ok ? 1 : 0;
 }
+extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCircuit c) { merkle_unit<false>(c); }
+extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle_bottom(DevCircuit c) { merkle_unit<true>(c); }
 
 // Latency mode (small batches, api.cpp): the same paths in the row form of the permutation
 // (rposeidon.h: 16 lanes per path, lane L < 12 holding word L), four paths per wave.  A path is a
