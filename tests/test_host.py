@@ -339,3 +339,15 @@ def test_shape_variant_limits():
             vk.shape_variant(npi, nf)
         assert e.value.code == p2v.E_SHAPE
     assert vk.shape_variant(0, 0).info.proof_words == vk.info.proof_words - 4 - 8
+
+
+def test_python_flag_constants_match_the_header():
+    """p2v.py's FLAG_* values are the P2V_FLAG_* macros of include/p2v.h (the ABI the ctypes
+    mirror passes through), including P2V_FLAG_LOOKAHEAD."""
+    import re
+    p2v = p2v_module()
+    hdr = open(os.path.join(ROOT, "include", "p2v.h")).read()
+    macros = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define P2V_FLAG_(\w+)\s+(\d+)u", hdr)}
+    assert {"INPUT_DEVICE", "RESULT_DEVICE", "NO_SYNC", "UNIT_FILTERS", "INPUT_TILED", "LOOKAHEAD"} <= set(macros)
+    for name, val in macros.items():
+        assert getattr(p2v, "FLAG_" + name) == val, name
