@@ -347,7 +347,7 @@ extern "C" __global__ void __launch_bounds__(256) k_leaf(DevCircuit c) {
 
 // ------------------------------------------------------------------------ Merkle paths
 #ifndef P2V_MERKLE_WAVES
-#define P2V_MERKLE_WAVES 6   // amdgpu_waves_per_eu on k_merkle: 77 VGPRs, 6 waves/SIMD, no scratch (serial +4.7 %, pipelined unchanged; 0 = compiler default, 5 waves)
+#define P2V_MERKLE_WAVES 6   // amdgpu_waves_per_eu on k_merkle: 77-79 VGPRs, 6 waves/SIMD, no scratch (serial +4.7 %, pipelined unchanged; 0 = compiler default, 5 waves)
 #endif
 #if P2V_MERKLE_WAVES > 0
 #define P2V_MERKLE_ATTR __attribute__((amdgpu_waves_per_eu(P2V_MERKLE_WAVES)))
