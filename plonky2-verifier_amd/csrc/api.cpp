@@ -137,6 +137,8 @@ struct p2v_verifier {
   // alternate runs; tr_done[s]: the transcript into buffer s is complete, chal_free[s]: the run
   // that read buffer s has completed (k_status)
   hipStream_t ts = nullptr;
+  hipStream_t side3 = nullptr;      // latency mode: the coset / misc vanishing kernels beside the Poseidon parts
+  hipEvent_t dep_v3 = nullptr;
   hipEvent_t tr_done[2] = {nullptr, nullptr}, chal_free[2] = {nullptr, nullptr};
   DevBuf chal2;
   unsigned la_seq = 0;
@@ -367,6 +369,8 @@ void p2v_verifier_free(p2v_verifier* v) {
   if (v->side) (void)hipStreamDestroy(v->side);
   if (v->side2) (void)hipStreamDestroy(v->side2);
   if (v->ts) (void)hipStreamDestroy(v->ts);
+  if (v->side3) (void)hipStreamDestroy(v->side3);
+  if (v->dep_v3) (void)hipEventDestroy(v->dep_v3);
   for (int k = 0; k < 2; k++) {
     if (v->tr_done[k]) (void)hipEventDestroy(v->tr_done[k]);
     if (v->chal_free[k]) (void)hipEventDestroy(v->chal_free[k]);
@@ -610,6 +614,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   // (the latency-mode and lookahead streams are created on first use: every stream a process
   // creates may take one of its few hardware queues, GPU_MAX_HW_QUEUES = 4, and two workspaces'
   // main and side streams must not share one)
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_v3, hipEventDisableTiming);
   for (int k = 0; k < 2 && e == hipSuccess; k++) {
     e = hipEventCreateWithFlags(&v->tr_done[k], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&v->chal_free[k], hipEventDisableTiming);
@@ -808,19 +813,31 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   T0(4, sd);
   // (one wave per work-group; the _r2 forms hold exactly the standard 2 challenge rounds)
   const bool r2 = d.r == 2;
+  // latency mode: the coset and misc items on a stream of their own, beside the Poseidon parts
+  // (each class is a handful of waves whose chain is the batch's tail)
+  hipStream_t sv = sd;
+  if (fri2) {
+    if (!v->side3) HCK(hipStreamCreateWithFlags(&v->side3, hipStreamNonBlocking));
+    HCK(hipStreamWaitEvent(v->side3, v->p1_done, 0));
+    sv = v->side3;
+  }
   if (d.vcls[1] > d.vcls[0]) {
     if (r2) k_vanish_poseidon_r2<<<(d.vcls[1] - d.vcls[0]) * NPB, 64, 0, sd>>>(d);
     else k_vanish_poseidon_rn<<<(d.vcls[1] - d.vcls[0]) * NPB, 64, 0, sd>>>(d);
   }
   DBG("k_vanish_poseidon", sd);
   if (d.vcls[2] > d.vcls[1]) {
-    if (r2) k_vanish_coset_r2<<<(d.vcls[2] - d.vcls[1]) * NPB, 64, 0, sd>>>(d);
-    else k_vanish_coset_rn<<<(d.vcls[2] - d.vcls[1]) * NPB, 64, 0, sd>>>(d);
+    if (r2) k_vanish_coset_r2<<<(d.vcls[2] - d.vcls[1]) * NPB, 64, 0, sv>>>(d);
+    else k_vanish_coset_rn<<<(d.vcls[2] - d.vcls[1]) * NPB, 64, 0, sv>>>(d);
   }
-  DBG("k_vanish_coset", sd);
-  if (r2) k_vanish_r2<<<(d.vcls[3] - d.vcls[2]) * NPB, 64, 0, sd>>>(d);
-  else k_vanish_rn<<<(d.vcls[3] - d.vcls[2]) * NPB, 64, 0, sd>>>(d);
-  DBG("k_vanish", sd);
+  DBG("k_vanish_coset", sv);
+  if (r2) k_vanish_r2<<<(d.vcls[3] - d.vcls[2]) * NPB, 64, 0, sv>>>(d);
+  else k_vanish_rn<<<(d.vcls[3] - d.vcls[2]) * NPB, 64, 0, sv>>>(d);
+  DBG("k_vanish", sv);
+  if (sv != sd) {
+    HCK(hipEventRecord(v->dep_v3, sv));
+    HCK(hipStreamWaitEvent(sd, v->dep_v3, 0));   // k_vanish_final sums every item
+  }
   if (d.vcls[4] > d.vcls[3]) {
     if (r2) k_vanish_lookup_r2<<<(d.vcls[4] - d.vcls[3]) * NPB, 64, 0, sd>>>(d);
     else k_vanish_lookup_rn<<<(d.vcls[4] - d.vcls[3]) * NPB, 64, 0, sd>>>(d);
