@@ -996,3 +996,27 @@ def test_gpu_mds_layer_carry_fixup(p2v):
             assert int(o[i]) % P == (al + (ah << 32)) % P, (i, s)
             fired += ((al + (ah >> 32) * 0xFFFFFFFF) >> 32) + (ah & 0xFFFFFFFF) >= 1 << 32   # the carry of reduce_rows
     assert fired > 300   # the fix-up branch really ran (hundreds of rows, in every group)
+
+
+def test_gpu_latency_and_batch_modes_interleaved(p2v):
+    """One workspace alternating between latency mode (n <= 64: row-form Merkle paths, k_fri and
+    the coset / misc vanishing kernels on lazily created streams of their own) and the batch
+    path (n > 64), on a lookup circuit so every vanishing class runs: each run's statuses and
+    traces equal the expected ones, whatever ran before it on the workspace."""
+    from test_real_circuits import _lookup_reject_cases
+    gc = gen_circuit(6, 4, 5, 1, 28, 16, 0, 1)
+    cases = _lookup_reject_cases(gc)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    packed = vk.pack_many([c[0] for c in cases])
+    want = np.array([c[1] for c in cases])
+    bv = p2v.BatchVerifier(vk, 0, 300)
+    ref_tr = {}
+    for n in (1, 300, 3, 64, 65, 1, 257, 2):
+        sel = np.arange(n) % len(cases)
+        res, tr = bv.run(np.ascontiguousarray(packed[sel]), trace=True)
+        assert np.array_equal(res, want[sel]), (n, res[:8], want[sel][:8])
+        for i in range(min(n, len(cases))):
+            if i in ref_tr:
+                assert np.array_equal(tr[i], ref_tr[i]), (n, i)
+            else:
+                ref_tr[i] = tr[i].copy()
