@@ -27,13 +27,7 @@ extern "C" __global__ void k_transcript_x(DevCircuit, int);
 extern "C" __global__ void k_leaf(DevCircuit);
 extern "C" __global__ void k_merkle(DevCircuit);
 extern "C" __global__ void k_merkle_row(DevCircuit);
-extern "C" __global__ void k_merkle_bottom(DevCircuit);
 extern "C" __global__ void k_fri(DevCircuit);
-extern "C" __global__ void k_mtask(DevCircuit);
-extern "C" __global__ void k_mtop(DevCircuit);
-extern "C" __global__ void k_mcheck(DevCircuit);
-extern "C" __global__ void k_mfix(DevCircuit);
-extern "C" __global__ void k_mcap(DevCircuit);
 extern "C" __global__ void k_vanish_r2(DevCircuit);
 extern "C" __global__ void k_vanish_rn(DevCircuit);
 extern "C" __global__ void k_vanish_poseidon_r2(DevCircuit);
@@ -58,9 +52,8 @@ int fail(int code, const std::string& msg) { g_err = msg; return code; }
 
 // per-kernel timing slots; k_fri and k_vanish run on the side stream, concurrently with k_merkle
 // (k_leaf + k_transcript: the split form of k_phase1, env P2V_PHASE1=split, measurement only)
-// (k_mtop: the shared top levels of the Merkle paths, k_mtop + k_mcheck + k_mfix, merkle.hip)
-const char* kKernelNames = "k_transpose,k_phase1,k_merkle,k_fri,k_vanish,k_status,k_vanish_final,k_lut,k_leaf,k_transcript,k_mtop";
-constexpr int kNumKernels = 11;
+const char* kKernelNames = "k_transpose,k_phase1,k_merkle,k_fri,k_vanish,k_status,k_vanish_final,k_lut,k_leaf,k_transcript";
+constexpr int kNumKernels = 10;
 
 struct DevBuf {
   void* p = nullptr;
@@ -120,9 +113,6 @@ struct p2v_verifier {
   DevCircuit dc{};
   std::vector<DevBuf> bufs;
   DevBuf in, soa, chal, leafdig, mk, fbits, qvals, van, vparts, lutre, lutpart, res, trace;
-  DevBuf mt_val, mt_cnt, mt_task, mt_fix, mt_flag;   // Merkle top levels (merkle.hip)
-  hipEvent_t dep_mt = nullptr;              // k_mtask done (side stream) -> k_mtop (main)
-  int merkle_trees = 0;                     // trees with k_merkle units (merkle_order prefix)
   DevBuf t_cs, t_kis, t_gkind, t_gpar, t_ggrp, t_gwoff, t_w, t_gs, t_ge, t_lin, t_lout, t_loff, t_llen, t_tw, t_ops, t_vit, t_rin, t_rout, t_roff, t_rch, t_pbase, t_pw;
   hipEvent_t ev[2 * kNumKernels];   // start/end per kernel
   hipEvent_t dep_p1 = nullptr, dep_side = nullptr, dep_tr = nullptr;
@@ -357,7 +347,7 @@ void p2v_verifier_free(p2v_verifier* v) {
   }
   (void)hipSetDevice(v->device);
   for (DevBuf* b : {&v->in, &v->soa, &v->chal, &v->leafdig, &v->mk, &v->fbits, &v->qvals, &v->van, &v->vparts, &v->lutre, &v->res, &v->trace, &v->t_cs, &v->t_kis,
-                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit, &v->t_rin, &v->t_rout, &v->t_roff, &v->t_rch, &v->t_pbase, &v->t_pw, &v->lutpart, &v->mt_val, &v->mt_cnt, &v->mt_task, &v->mt_fix, &v->mt_flag, &v->chal2, &v->j_blob, &v->j_offs, &v->j_skel, &v->j_tok, &v->j_ok,
+                    &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit, &v->t_rin, &v->t_rout, &v->t_roff, &v->t_rch, &v->t_pbase, &v->t_pw, &v->lutpart, &v->chal2, &v->j_blob, &v->j_offs, &v->j_skel, &v->j_tok, &v->j_ok,
                     &v->b_rsrc, &v->b_rdst, &v->b_rlen, &v->b_coff, &v->b_cval})
     b->free_();
   if (v->timed) for (auto& e : v->ev) (void)hipEventDestroy(e);
@@ -365,7 +355,6 @@ void p2v_verifier_free(p2v_verifier* v) {
   if (v->dep_side) (void)hipEventDestroy(v->dep_side);
   if (v->dep_tr) (void)hipEventDestroy(v->dep_tr);
   if (v->p1_done) (void)hipEventDestroy(v->p1_done);
-  if (v->dep_mt) (void)hipEventDestroy(v->dep_mt);
   if (v->side) (void)hipStreamDestroy(v->side);
   if (v->side2) (void)hipStreamDestroy(v->side2);
   if (v->ts) (void)hipStreamDestroy(v->ts);
@@ -410,12 +399,6 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (const char* ff = getenv("P2V_FRI_FIRST")) v->fri_first = ff[0] == '1';
   if (const char* sw = getenv("P2V_SIDE_WG")) v->side_wg = atoi(sw) == 64 ? 64 : 256;
   if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : 0;
-  // Merkle levels below the cap computed once per distinct node of a proof (merkle.hip); env
-  // P2V_MTOP_K = K > 0 turns it on.  Off by default: measured 1.105 M against 1.129 M proofs/s
-  // pipelined (K = 5; profiles/r03g_merkle_shared.txt): the 11 % fewer compressions do not pay
-  // for the task lists, the gathered loads and the extra launches
-  int mtop_k = 0;
-  if (const char* mk = getenv("P2V_MTOP_K")) mtop_k = atoi(mk);
   DevCircuit& d = v->dc;
   memset(&d, 0, sizeof d);
   d.r = C.r; d.Q = C.num_queries; d.S = (int)C.arities.size(); d.T = 4 + d.S;
@@ -432,36 +415,12 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   d.o_zs = L.o_zs; d.o_pp = L.o_pp; d.o_quot = L.o_quot; d.o_lzs = L.o_lzs; d.o_zs_next = L.o_zs_next; d.o_lzs_next = L.o_lzs_next;
   d.n_this = L.n_this; d.n_next = L.n_next; d.ccaps = L.ccaps; d.final_poly = L.final_poly; d.pow = L.pow; d.q0 = L.q0; d.qstride = L.qstride;
   for (int t = 0; t < 4; t++) { d.leaf[t] = L.leaf[t]; d.path[t] = L.path[t]; }
-  // Merkle top levels: K_t = min(mt_K, depth_t) per tree (a tree whose paths end below the cap
-  // level, depth 0, keeps the whole check in k_merkle); tasks encode q in 8 bits
-  d.mt_K = (mtop_k > 0 && C.num_queries <= 255) ? std::min(mtop_k, 16) : 0;
-  d.mt_L = C.lde_bits - C.cap_height;
-  int& merkle_trees = v->merkle_trees;
-  {
-    int ncls = 0;
-    memset(d.mt_kcls, -1, sizeof d.mt_kcls);
-    for (int t = 0; t < d.T; t++) {
-      const int dep = t < 4 ? C.depth0 : C.step_depth[t - 4];
-      const int K = (d.mt_K > 0 && dep > 0) ? std::min(d.mt_K, dep) : 0;
-      d.mt_k[t] = (int8_t)K;
-      if (K > 0 && d.mt_kcls[K] < 0) { d.mt_kcls[K] = (int8_t)ncls; d.mt_kval[ncls++] = (int8_t)K; }
-    }
-    d.mt_ncls = ncls;
-    d.mt_nbuckets = ncls * (d.mt_K + 1);
-    if (ncls == 0) d.mt_K = 0;
-  }
   {   // unit orders: most expensive tree first (stable), see DevCircuit::leaf_order
     std::vector<std::pair<int64_t, int>> lc, mc;
-    merkle_trees = 0;
     for (int t = 0; t < d.T; t++) {
       const int64_t len = t < 4 ? C.leaf_width[t] : (2ll << C.arities[t - 4]);
       lc.push_back({-(len + 7) / 8, t});
-      const int bottom = (t < 4 ? C.depth0 : C.step_depth[t - 4]) - d.mt_k[t];
-      // a tree whose every level is shared (bottom 0, K_t > 0) has no k_merkle units: it sorts
-      // last and the grid stops before it (a depth-0 tree, K_t = 0, keeps its cap check there)
-      const bool none = bottom == 0 && d.mt_k[t] > 0;
-      mc.push_back({none ? 1 : -(int64_t)bottom, t});
-      if (!none) merkle_trees++;
+      mc.push_back({-(int64_t)(t < 4 ? C.depth0 : C.step_depth[t - 4]), t});
     }
     std::stable_sort(lc.begin(), lc.end()); std::stable_sort(mc.begin(), mc.end());
     for (int k = 0; k < d.T; k++) { d.leaf_order[k] = (int8_t)lc[k].second; d.merkle_order[k] = (int8_t)mc[k].second; }
@@ -588,11 +547,6 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (e == hipSuccess) e = v->vparts.alloc((size_t)d.n_vitems * 2 * d.r * B * 8);
   if (e == hipSuccess) e = v->lutre.alloc((size_t)d.r * (d.nluts ? d.nluts : 1) * B * 8);
   if (e == hipSuccess) e = v->lutpart.alloc((size_t)d.r * (d.n_lut_pieces ? d.n_lut_pieces : 1) * B * 8);
-  if (e == hipSuccess && d.mt_K > 0) e = v->mt_val.alloc((size_t)d.mt_K * d.Q * d.T * 4 * B * 8);
-  if (e == hipSuccess && d.mt_K > 0) e = v->mt_cnt.alloc((size_t)(d.mt_nbuckets + 1) * 4);
-  if (e == hipSuccess && d.mt_K > 0) e = v->mt_task.alloc((size_t)d.mt_nbuckets * B * d.Q * 4);
-  if (e == hipSuccess && d.mt_K > 0) e = v->mt_fix.alloc((size_t)B * d.T * 4);
-  if (e == hipSuccess && d.mt_K > 0) e = v->mt_flag.alloc((size_t)B * d.T * 4);
   if (e == hipSuccess) e = v->res.alloc(B);
   if (e == hipSuccess) e = hipHostMalloc((void**)&v->h_res, B);
   if (e == hipSuccess) e = v->trace.alloc((size_t)C.trace_words * B * 8);
@@ -601,7 +555,6 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_side, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_tr, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->p1_done, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_mt, hipEventDisableTiming);
   // the side stream carries few, long-latency waves (vanishing items, FRI queries); a
   // high-priority queue for it was measured (P2V_SIDE_PRIO=1) and changed nothing
   if (e == hipSuccess) {
@@ -628,7 +581,6 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   d.lut_rin = (const uint32_t*)v->t_rin.p; d.lut_rout = (const uint32_t*)v->t_rout.p; d.lut_roff = (const int64_t*)v->t_roff.p; d.lut_rchunks = (const int32_t*)v->t_rch.p; d.lut_pbase = (const int32_t*)v->t_pbase.p;
   d.twiddles = (const uint64_t*)v->t_tw.p; d.tops = (const int32_t*)v->t_ops.p; d.vitems = (const int32_t*)v->t_vit.p;
   d.pos_w = (const uint64_t*)v->t_pw.p;
-  d.mt_val = (uint64_t*)v->mt_val.p; d.mt_cnt = (int32_t*)v->mt_cnt.p; d.mt_task = (uint32_t*)v->mt_task.p; d.mt_fix = (uint32_t*)v->mt_fix.p; d.mt_flag = (int32_t*)v->mt_flag.p;
   d.soa = (const uint64_t*)v->soa.p; d.chal = (uint64_t*)v->chal.p; d.leafdig = (uint64_t*)v->leafdig.p; d.mk_ok = (uint8_t*)v->mk.p;
   d.fri_bits = (uint32_t*)v->fbits.p; d.qvals = (uint64_t*)v->qvals.p; d.van = (uint64_t*)v->van.p; d.vparts = (uint64_t*)v->vparts.p; d.lutre = (uint64_t*)v->lutre.p; d.lutpart = (uint64_t*)v->lutpart.p;
   *out = v;
@@ -797,14 +749,6 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     DBG("k_fri", sd);
     T1(3, sd);
   }
-  // Merkle top levels: the per-proof task lists first on the side stream (k_mtop waits for them)
-  if (d.mt_K > 0) {
-    HCK(hipMemsetAsync(d.mt_cnt, 0, (size_t)(d.mt_nbuckets + 1) * 4, sd));
-    HCK(hipMemsetAsync(d.mt_flag, 0, (size_t)d.T * d.B * 4, sd));
-    k_mtask<<<(d.Q * NPB + 3) / 4, 256, 0, sd>>>(d);
-    DBG("k_mtask", sd);
-    if (sd != st) HCK(hipEventRecord(v->dep_mt, sd));
-  }
   T0(7, sd);
   if (d.n_lut_pieces > 0) k_lut<<<(d.r * d.n_lut_pieces * NPB + 3) / 4, 256, 0, sd>>>(d);
   DBG("k_lut", sd);
@@ -856,32 +800,11 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   }
   if (sd != st) HCK(hipEventRecord(v->dep_side, sd));
   T0(2, st);
-  const int merkle_units = d.Q * v->merkle_trees * NPB;
-  if (lat && d.mt_K == 0) k_merkle_row<<<(unsigned)(((int64_t)d.Q * d.T * d.n * 16 + 255) / 256), 256, 0, st>>>(d);
-  else if (merkle_units > 0 && d.mt_K > 0) k_merkle_bottom<<<(merkle_units + 3) / 4, 256, 0, st>>>(d);
-  else if (merkle_units > 0) k_merkle<<<(merkle_units + 3) / 4, 256, 0, st>>>(d);
+  const int merkle_units = d.Q * d.T * NPB;
+  if (lat) k_merkle_row<<<(unsigned)(((int64_t)d.Q * d.T * d.n * 16 + 255) / 256), 256, 0, st>>>(d);
+  else k_merkle<<<(merkle_units + 3) / 4, 256, 0, st>>>(d);
   DBG("k_merkle", st);
   T1(2, st);
-  if (d.mt_K > 0) {
-    if (sd != st) HCK(hipStreamWaitEvent(st, v->dep_mt, 0));
-    T0(10, st);
-    // one wave per task chunk: the bound per tree is n Q / 64 + K_t (each of its K_t buckets
-    // rounds up once); the waves past the actual chunk count exit at once
-    int64_t chunks = 0;
-    for (int t = 0; t < d.T; t++) if (d.mt_k[t] > 0) chunks += (int64_t)d.n * d.Q / 64 + d.mt_k[t];
-    k_mtop<<<(unsigned)((chunks + 3) / 4), 256, 0, st>>>(d);
-    DBG("k_mtop", st);
-    int top_trees = 0;
-    for (int t = 0; t < d.T; t++) top_trees += d.mt_k[t] > 0;
-    const unsigned top_groups = (unsigned)((top_trees * d.Q * NPB + 3) / 4);
-    k_mcheck<<<top_groups, 256, 0, st>>>(d);
-    DBG("k_mcheck", st);
-    k_mcap<<<top_groups, 256, 0, st>>>(d);
-    DBG("k_mcap", st);
-    k_mfix<<<64, 256, 0, st>>>(d);
-    DBG("k_mfix", st);
-    T1(10, st);
-  }
   if (sd != st) HCK(hipStreamWaitEvent(st, v->dep_side, 0));
   if (fri2) HCK(hipStreamWaitEvent(st, v->dep_fri, 0));
   T0(5, st);

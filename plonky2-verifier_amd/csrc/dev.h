@@ -69,18 +69,6 @@ struct DevCircuit {
   const int32_t* vitems;           // vanishing work items [n_vitems][4] = {VI_*, a, b, first term}
   int32_t n_vitems;
   int32_t vcls[5];                 // item ranges of the vanishing kernel classes (Poseidon, coset, misc, lookup)
-  // Merkle top levels shared per proof (merkle.hip): mt_K levels below the cap (0: off), the cap's
-  // absolute level mt_L = lde_bits - cap_height, per tree K_t = min(mt_K, depth_t) (0: the whole
-  // path in k_merkle), the distinct K_t values (task classes) and their buffers
-  int32_t mt_K, mt_L, mt_ncls, mt_nbuckets;
-  int8_t mt_k[4 + P2V_MAX_STEPS];
-  int8_t mt_kcls[33];              // K -> class
-  int8_t mt_kval[4 + P2V_MAX_STEPS];   // class -> K
-  uint64_t* mt_val;                // [mt_K][Q][T][4][B]: chain values at levels mt_L - mt_K + 1 ..
-  int32_t* mt_cnt;                 // [mt_nbuckets] task counts, then the count of listed (proof, tree) pairs
-  uint32_t* mt_task;               // [mt_nbuckets][B * Q]: (p << 8) | q
-  uint32_t* mt_fix;                // [B * T]: (p << 8) | t
-  int32_t* mt_flag;                // [T][B]: the (proof, tree) failed an equality check
   const uint64_t* pos_w;           // PoseidonGate part 3: W = A'M [12][12] then k = A' rc [12] (vanish_poseidon.hip)
   // batch buffers
   const uint64_t* soa;             // [words][B]

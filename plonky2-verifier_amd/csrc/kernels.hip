@@ -354,10 +354,6 @@ extern "C" __global__ void __launch_bounds__(256) k_leaf(DevCircuit c) {
 #else
 #define P2V_MERKLE_ATTR
 #endif
-// BOTTOM: with the top levels shared per proof (merkle.hip, opt-in), the paths stop K_t levels
-// below the cap and leave that node in leafdig for k_mtop / k_mcheck (a kernel of its own, so
-// that the default k_merkle keeps its 77 VGPRs and no scratch)
-template <bool BOTTOM>
 __device__ __forceinline__ void merkle_unit(const DevCircuit& c) {
   const int lane = threadIdx.x & 63;
   const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -377,7 +373,6 @@ __device__ __forceinline__ void merkle_unit(const DevCircuit& c) {
     idx >>= sh; depth = c.step_depth[s]; poff = base + c.step_path[s];
   }
   uint64_t* src = c.leafdig + ((int64_t)(q * c.T + t) * 4) * c.B + p;
-  if constexpr (BOTTOM) depth -= c.mt_k[t];
   uint64_t cur[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) cur[i] = src[(int64_t)i * c.B];
@@ -396,11 +391,6 @@ __device__ __forceinline__ void merkle_unit(const DevCircuit& c) {
     for (int i = 0; i < 4; i++) cur[i] = st[i];
     idx >>= 1;
   }
-  if constexpr (BOTTOM) {
-#pragma unroll
-    for (int i = 0; i < 4; i++) src[(int64_t)i * c.B] = cur[i];
-    return;
-  }
   // cap_roots !! (idx >> depth)
   bool ok = idx < (uint32_t)c.cap_len;
   const uint32_t ci = ok ? idx : 0;
@@ -416,8 +406,7 @@ __device__ __forceinline__ void merkle_unit(const DevCircuit& c) {
   }
   c.mk_ok[(int64_t)(q * c.T + t) * c.B + p] = ok ? 1 : 0;
 }
-extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCircuit c) { merkle_unit<false>(c); }
-extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle_bottom(DevCircuit c) { merkle_unit<true>(c); }
+extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCircuit c) { merkle_unit(c); }
 
 // Latency mode (small batches, api.cpp): the same paths in the row form of the permutation
 // (rposeidon.h: 16 lanes per path, lane L < 12 holding word L), four paths per wave.  A path is a

@@ -355,10 +355,10 @@ def test_gpu_random_number_mutations_vs_oracle(p2v, nb, mode, lk):
 
 
 def _merkle_top_cases(gc, base_txt, qidx, info, rnd, n_random=40):
-    """Mutations aimed at the Merkle levels shared per proof (merkle.hip): siblings in the top
-    min(5, depth) levels of representatives and of non-representatives, the same sibling changed
-    identically in two queries on one node, bottom values (leaf evaluations), and random
-    single / double sibling changes in the shared levels."""
+    """Mutations aimed at the top Merkle levels, where a proof's query paths meet: siblings in
+    the top min(5, depth) levels of the lowest query on a node and of another query on the same
+    node, the same sibling changed identically in two queries on one node, bottom values (leaf
+    evaluations), and random single / double sibling changes in those levels."""
     base = json.loads(base_txt)
     Q = len(qidx)
     lt = info.lde_bits - info.cap_height
@@ -429,13 +429,13 @@ def _merkle_top_cases(gc, base_txt, qidx, info, rnd, n_random=40):
 
 
 @pytest.mark.parametrize("nb", [6, 8, 12])
-def test_gpu_merkle_shared_levels_vs_oracle(p2v, nb):
-    """The top Merkle levels computed once per distinct node of a proof (merkle.hip: k_mtask,
-    k_mtop, k_mcheck, k_mfix) against the oracle's per-path verification (Hash/Merkle.hs:27-42):
-    mutations of representatives' and non-representatives' siblings in the shared levels, the
-    same change in two queries on one node, bottom values, random changes.  n = 6: every level of
-    every path is shared (depth 5); n = 8 and 12: k_merkle's bottom levels below them.  Every
-    status and trace word equals the oracle's; the campaign reaches the Merkle failure classes."""
+def test_gpu_merkle_top_level_mutations_vs_oracle(p2v, nb):
+    """Merkle paths near the cap against the oracle's per-path verification
+    (Hash/Merkle.hs:27-42): mutations of siblings on nodes shared by several queries of one
+    proof, the same change in two queries on one node, bottom values, random changes.  Every
+    status and trace word equals the oracle's; the campaign reaches the Merkle failure classes.
+    (Round 3's opt-in path that computed these shared levels once per node was removed in
+    round 4; the campaign now holds k_merkle.)"""
     import random
     from support import trace_offsets
     O = oracle()
@@ -448,17 +448,7 @@ def test_gpu_merkle_shared_levels_vs_oracle(p2v, nb):
     off = trace_offsets(info.num_challenges, info.num_fri_steps, info.num_query_rounds)["query_idx"]
     qidx = [int(x) for x in tr[off: off + info.num_query_rounds]]
     cases = [base] + _merkle_top_cases(gc, base, qidx, info, random.Random(nb))
-    # the sharing is opt-in (P2V_MTOP_K, read when a verifier is created); K = 5 and K = 3
-    old = os.environ.get("P2V_MTOP_K")
-    try:
-        for k in ("5", "3"):
-            os.environ["P2V_MTOP_K"] = k
-            sts, _ = _gpu_vs_oracle(p2v, gc, cases)
-    finally:
-        if old is None:
-            os.environ.pop("P2V_MTOP_K", None)
-        else:
-            os.environ["P2V_MTOP_K"] = old
+    sts, _ = _gpu_vs_oracle(p2v, gc, cases)
     assert {-1, -2} <= set(sts), sorted(set(sts))
 
 
