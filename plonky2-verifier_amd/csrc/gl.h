@@ -68,6 +68,10 @@ GL_HD uint64_t reduce96_nc(uint64_t hi, uint64_t lo) {
   return r;
 }
 
+#ifndef P2V_MUL_PRODUCT
+#define P2V_MUL_PRODUCT 1   // device multiply's partial products: 1 = chained MAD addends (round 4), 0 = carry adds
+#endif
+
 #if defined(__HIP_DEVICE_COMPILE__)
 // gfx950 carry-chain primitives.  The compiler does not use the carry-out of
 // v_mad_u64_u32 / v_add_co_u32 and re-derives every carry with a 64-bit compare; these
@@ -77,6 +81,8 @@ GL_HD uint64_t reduce96_nc(uint64_t hi, uint64_t lo) {
 namespace ax {
 __device__ __forceinline__ uint64_t mad0(uint32_t a, uint32_t b) { uint64_t d, c; asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(d), "=s"(c) : "v"(a), "v"(b)); return d; }
 __device__ __forceinline__ uint64_t mad_co(uint32_t a, uint32_t b, uint64_t x, uint64_t& co) { uint64_t d; asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(a), "v"(b), "v"(x)); return d; }
+// a b + x where the caller guarantees no carry out of 64 bits
+__device__ __forceinline__ uint64_t mad_nc(uint32_t a, uint32_t b, uint64_t x) { uint64_t co; return mad_co(a, b, x, co); }
 __device__ __forceinline__ uint64_t madm1_co(uint32_t a, uint64_t x, uint64_t& co) { uint64_t d; asm("v_mad_u64_u32 %0, %1, %2, -1, %3" : "=v"(d), "=s"(co) : "v"(a), "v"(x)); return d; }
 __device__ __forceinline__ uint32_t add_co(uint32_t a, uint32_t b, uint64_t& co) { uint32_t d; asm("v_add_co_u32_e64 %0, %1, %2, %3" : "=v"(d), "=s"(co) : "v"(a), "v"(b)); return d; }
 __device__ __forceinline__ uint32_t addc_co(uint32_t a, uint32_t b, uint64_t ci, uint64_t& co) { uint32_t d; asm("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(d), "=s"(co) : "v"(a), "v"(b), "s"(ci)); return d; }
@@ -104,6 +110,22 @@ __device__ __forceinline__ uint64_t mul_nc_dev_v(uint64_t a, uint64_t b) {
   using namespace ax;
   const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
   uint64_t cm, c1, c2, ct, c4, bw1, bw2, bw3, bw4;
+#if P2V_MUL_PRODUCT == 1
+  // the partial products chained through the MADs' 64-bit addends: every carry between the
+  // 32-bit columns is absorbed by the next MAD, so no add-with-carry is needed
+  //   x = a0 b1 + hi(a0 b0)          <= (2^32-1)^2 + 2^32 - 2 < 2^64
+  //   y = a1 b0 + x = y + cm 2^64    (the column of weight 2^32; cm has weight 2^96)
+  //   h = a1 b1 + hi(y)              <= (2^32-1)^2 + 2^32 - 1 < 2^64
+  // product = lo(a0 b0) + lo(y) 2^32 + h 2^64 + cm 2^96: 4 MADs and 2 zero-extensions against
+  // 4 MADs and 3 carry adds (round 4)
+  (void)c1; (void)c2;
+  const uint64_t p00 = mad0(a0, b0);
+  const uint64_t x = mad_nc(a0, b1, p00 >> 32);
+  const uint64_t y = mad_co(a1, b0, x, cm);
+  const uint64_t hh = mad_nc(a1, b1, y >> 32);
+  const uint32_t h0 = (uint32_t)hh, h1 = (uint32_t)(hh >> 32);          // + cm: below
+  const uint64_t lo = ((uint64_t)(uint32_t)y << 32) | (uint32_t)p00;
+#else
   const uint64_t p00 = mad0(a0, b0);
   const uint64_t p01 = mad0(a0, b1);
   const uint64_t m = mad_co(a1, b0, p01, cm);   // a0 b1 + a1 b0 = m + cm 2^64
@@ -112,6 +134,7 @@ __device__ __forceinline__ uint64_t mul_nc_dev_v(uint64_t a, uint64_t b) {
   const uint32_t h0 = addc_co((uint32_t)p11, (uint32_t)(m >> 32), c1, c2);
   const uint32_t h1 = addc0((uint32_t)(p11 >> 32), c2);                 // + cm: below
   const uint64_t lo = ((uint64_t)lo1 << 32) | (uint32_t)p00;
+#endif
   if constexpr (V == 2) {
   // as below, but the -2^64 case (only when the product has bits 64..95 zero and bits 0..63
   // below 2^32, e.g. powers of two) is a wave-uniform branch that is almost never taken

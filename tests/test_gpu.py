@@ -894,6 +894,17 @@ def test_gpu_field_mul_edge_values(p2v):
         out = p2v.device_selftest(op, a, b)
         bad = np.nonzero(out != exp)[0]
         assert len(bad) == 0, [(op, hex(int(a[i])), hex(int(b[i])), hex(int(out[i])), hex(int(exp[i]))) for i in bad[:5]]
+    # squares (two of the S-box's four products, Hash/Poseidon.hs:92-96): every combination of
+    # extreme 32-bit halves (the chained MAD addends' bounds are tight at halves 2^32 - 1),
+    # the edge values and random values
+    halves = [0, 1, 2, 0x7FFFFFFF, 0x80000000, 0xFFFFFFFE, 0xFFFFFFFF]
+    sq = [h1 << 32 | h0 for h1 in halves for h0 in halves] + ev + [int(x) for x in rng.integers(0, 1 << 64, size=4096, dtype=np.uint64)]
+    s = np.array(sq, dtype=np.uint64)
+    exp = np.array([(x * x) % P for x in sq], dtype=np.uint64)
+    for op in (0, 3):
+        out = p2v.device_selftest(op, s, s)
+        bad = np.nonzero(out != exp)[0]
+        assert len(bad) == 0, [(op, hex(int(s[i])), hex(int(out[i])), hex(int(exp[i]))) for i in bad[:5]]
 
 
 def test_gpu_poseidon_permutation_vs_oracle(p2v):
