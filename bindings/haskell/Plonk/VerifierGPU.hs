@@ -276,50 +276,67 @@ verifyWithCircuit (GpuCircuit fc) devices proofs = withForeignPtr fc $ \c -> do
 -- | One proof whose public-input / final-polynomial lengths differ from the circuit's.
 verifyShapeVariant :: Ptr P2vCircuit -> Int -> ProofWithPublicInputs -> IO Int8
 verifyShapeVariant c dev p = withArrayLen (proofWords p) $ \m ws ->
-  alloca $ \np -> alloca $ \nf -> alloca $ \out -> do
-    rc <- c_proof_shape_words ws (fromIntegral m) np nf
-    when (rc /= 0) $ throwLast "p2v_proof_shape_words"
-    a <- peek np
-    b <- peek nf
-    rc2 <- c_circuit_shape_variant c a b out
-    when (rc2 /= 0) $ throwLast "p2v_circuit_shape_variant"
-    v <- peek out
-    flip finally (c_circuit_free_now v) $ do
-      pwv <- infoProofWords v
-      allocaArray (fromIntegral pwv) $ \buf -> alloca $ \r -> do
-        rc3 <- c_pack_proof_words v ws (fromIntegral m) buf
-        when (rc3 /= 0) $ throwLast "p2v_pack_proof_words"
-        rc4 <- c_verify_batch v buf 1 r (fromIntegral dev)
-        when (rc4 /= 0) $ throwLast "p2v_verify_batch"
-        peek r
+  withShapeVariant c ws m $ \v -> do
+    pwv <- infoProofWords v
+    allocaArray (fromIntegral pwv) $ \buf -> alloca $ \r -> do
+      rc3 <- c_pack_proof_words v ws (fromIntegral m) buf
+      when (rc3 /= 0) $ throwLast "p2v_pack_proof_words"
+      rc4 <- c_verify_batch v buf 1 r (fromIntegral dev)
+      when (rc4 /= 0) $ throwLast "p2v_verify_batch"
+      peek r
+
+-- | The circuit's shape variant for the public-input / final-polynomial lengths of a
+-- word-encoded proof (p2v_proof_shape_words, p2v_circuit_shape_variant), freed afterwards.
+withShapeVariant :: Ptr P2vCircuit -> Ptr Word64 -> Int -> (Ptr P2vCircuit -> IO a) -> IO a
+withShapeVariant c ws m k = alloca $ \np -> alloca $ \nf -> alloca $ \out -> do
+  rc <- c_proof_shape_words ws (fromIntegral m) np nf
+  when (rc /= 0) $ throwLast "p2v_proof_shape_words"
+  a <- peek np
+  b <- peek nf
+  rc2 <- c_circuit_shape_variant c a b out
+  when (rc2 /= 0) $ throwLast "p2v_circuit_shape_variant"
+  v <- peek out
+  k v `finally` c_circuit_free_now v
 
 --------------------------------------------------------------------------------
 -- * Intermediates (the per-proof debug trace, include/p2v.h "debug trace layout")
 
 -- | The packed proof's trace words, with (r, S, Q, has_lookups), computed on GPU 0 by the same
--- kernels as 'verifyProof'.
+-- kernels as 'verifyProof'.  A proof with other public-input / final-polynomial lengths than the
+-- circuit implies is traced on the circuit's shape variant, as 'verifyWithCircuit' verifies it
+-- (the reference's proofChallenges reads both lists at any length).
 traceOf :: VerifierCircuitData -> ProofWithPublicInputs -> IO ((Int, Int, Int, Bool), [Word64])
 traceOf vkey proof = do
   GpuCircuit fc <- loadGpuCircuit vkey
-  withForeignPtr fc $ \c -> do
-    (r, s, q, lk, pw, tw) <- allocaBytes infoBytes $ \info -> do
-      rc <- c_circuit_get_info c info
-      when (rc /= 0) $ throwLast "p2v_circuit_get_info"
-      let i32 o = fromIntegral <$> (peekByteOff info o :: IO Int32)
-          i64 o = fromIntegral <$> (peekByteOff info o :: IO Int64)
-      (,,,,,) <$> i32 infoNumChallengesOffset <*> i32 infoNumFriStepsOffset <*> i32 infoNumQueryRoundsOffset
-              <*> ((/= (0 :: Int)) <$> i32 infoHasLookupsOffset) <*> i64 infoProofWordsOffset <*> i64 infoTraceWordsOffset
-    allocaArray pw $ \buf -> allocaArray tw $ \tr -> alloca $ \res -> alloca $ \vp -> do
-      withArrayLen (proofWords proof) $ \m ws -> do
-        rc <- c_pack_proof_words c ws (fromIntegral m) buf
-        when (rc /= 0) $ throwLast "p2v_pack_proof_words"
-      rc <- c_verifier_create c 0 1 vp
-      when (rc /= 0) $ throwLast "p2v_verifier_create"
+  withForeignPtr fc $ \c -> withArrayLen (proofWords proof) $ \m ws -> do
+    t <- traceWith c ws m
+    case t of
+      Just x  -> pure x
+      Nothing -> withShapeVariant c ws m $ \v ->
+        traceWith v ws m >>= maybe (throwLast "p2v_pack_proof_words") pure
+
+-- | The trace of one word-encoded proof on circuit c; Nothing when its lengths do not fit c's
+-- packed layout (P2V_E_SHAPE).
+traceWith :: Ptr P2vCircuit -> Ptr Word64 -> Int -> IO (Maybe ((Int, Int, Int, Bool), [Word64]))
+traceWith c ws m = do
+  (r, s, q, lk, pw, tw) <- allocaBytes infoBytes $ \info -> do
+    rc <- c_circuit_get_info c info
+    when (rc /= 0) $ throwLast "p2v_circuit_get_info"
+    let i32 o = fromIntegral <$> (peekByteOff info o :: IO Int32)
+        i64 o = fromIntegral <$> (peekByteOff info o :: IO Int64)
+    (,,,,,) <$> i32 infoNumChallengesOffset <*> i32 infoNumFriStepsOffset <*> i32 infoNumQueryRoundsOffset
+            <*> ((/= (0 :: Int)) <$> i32 infoHasLookupsOffset) <*> i64 infoProofWordsOffset <*> i64 infoTraceWordsOffset
+  allocaArray pw $ \buf -> allocaArray tw $ \tr -> alloca $ \res -> alloca $ \vp -> do
+    rc <- c_pack_proof_words c ws (fromIntegral m) buf
+    if rc == eShape then pure Nothing else do
+      when (rc /= 0) $ throwLast "p2v_pack_proof_words"
+      rc1 <- c_verifier_create c 0 1 vp
+      when (rc1 /= 0) $ throwLast "p2v_verifier_create"
       v <- peek vp
       rc2 <- c_verifier_run v buf 1 res tr nullPtr 0
       c_verifier_free v
       when (rc2 /= 0) $ throwLast "p2v_verifier_run"
-      (,) (r, s, q, lk) <$> peekArray tw tr
+      Just . (,) (r, s, q, lk) <$> peekArray tw tr
 
 -- | 'Challenge.Verifier.proofChallenges' (src/Challenge/Verifier.hs:58): same type, the
 -- challenges as the GPU transcript derives them.

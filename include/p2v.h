@@ -208,7 +208,8 @@ int  p2v_circuit_shape_variant(const p2v_circuit* c, int num_public_inputs, int 
                                        call is made (nothing queued on `stream` still writes it), so its transcript
                                        may run ahead of this workspace's earlier batches, on a stream of its own
                                        with a second challenge buffer, overlapping their Merkle / FRI work
-                                       (DESIGN.md §5.2); results are unchanged                                  */
+                                       (DESIGN.md §5.2); results are unchanged.  A measurement build that
+                                       transposes the batch (P2V_PROOF_MAJOR=0) rejects it with P2V_E_ARG   */
 #define P2V_FLAG_UNIT_FILTERS  8u  /* parity mode: every gate filter and lookup selector := 1, so the
                                       trace's combined values C_i expose every constraint program
                                       (the oracle's or_verify full_trace bit 1); statuses are then

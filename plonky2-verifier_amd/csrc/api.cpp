@@ -615,6 +615,9 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   d.tiled = (flags & P2V_FLAG_INPUT_TILED) ? 1 : 0;
   d.wstride = d.tiled ? 64 : 1;
   if (d.tiled && !P2V_PROOF_MAJOR) return fail(P2V_E_ARG, "P2V_FLAG_INPUT_TILED needs the in-place build (P2V_PROOF_MAJOR=1)");
+  // the lookahead transcript runs on its own stream and reads the batch in place; the transposing
+  // build's k_transpose writes v->soa on the caller's stream, which that stream does not wait for
+  if ((flags & P2V_FLAG_LOOKAHEAD) && !P2V_PROOF_MAJOR) return fail(P2V_E_ARG, "P2V_FLAG_LOOKAHEAD needs the in-place build (P2V_PROOF_MAJOR=1)");
   d.B = (int)((n + 63) / 64 * 64);
   const int64_t words = C.L.words;
   const uint64_t* src = proofs;
@@ -654,14 +657,16 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   const int nt_blocks = (tl * d.B + 255) / 256;
   const int leaf_units = d.Q * d.T * NPB;
   // staggered workspaces (p2v_verifier_chain): phase 1 after the linked workspace's latest one
+  bool chained = false;   // read under the lock: chain links may change from other host threads
   {
     std::lock_guard<std::mutex> lk(g_chain_mu);   // the linked workspace cannot be freed meanwhile
+    chained = v->chain_prev != nullptr;
     if (v->chain_prev && v->chain_prev->p1_recorded.load(std::memory_order_acquire))
       HCK(hipStreamWaitEvent(st, v->chain_prev->p1_done, 0));
   }
   // transcript lookahead: the transcript on v->ts into the challenge buffer of this run's parity,
   // after the run that last read that buffer; the leaf hashing on st; k_merkle after both
-  const bool la = (flags & P2V_FLAG_LOOKAHEAD) && (flags & P2V_FLAG_INPUT_DEVICE) && sd != st && !v->chain_prev;
+  const bool la = (flags & P2V_FLAG_LOOKAHEAD) && (flags & P2V_FLAG_INPUT_DEVICE) && sd != st && !chained;
   int la_slot = 0;
   if (la) {
     if (!v->ts) HCK(hipStreamCreateWithFlags(&v->ts, hipStreamNonBlocking));

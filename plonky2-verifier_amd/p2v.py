@@ -580,6 +580,13 @@ def verify_proof(vkey: VerifierCircuitData, proof: Union[ProofWithPublicInputs, 
     return _status_to_bool(int(res[0]))
 
 
+def _pack_error(vkey: VerifierCircuitData, text: bytes) -> str:
+    """The host packer's message for one proof that does not pack against `vkey`."""
+    out = np.empty(vkey.info.proof_words, dtype=np.uint64)
+    rc = lib().p2v_pack_proof_json(vkey.handle, text, len(text), out.ctypes.data)
+    return lib().p2v_last_error_message().decode(errors="replace") if rc != E_OK else "ok"
+
+
 def verify_proof_batch(vkey: VerifierCircuitData, proofs: Iterable[Union[ProofWithPublicInputs, str, bytes]],
                        device: int = 0) -> List[Union[bool, VerifierError]]:
     """Batch form: one entry per proof, True/False or the VerifierError the reference would raise.
@@ -588,14 +595,36 @@ def verify_proof_batch(vkey: VerifierCircuitData, proofs: Iterable[Union[ProofWi
     texts = [p.json if isinstance(p, ProofWithPublicInputs) else _bytes(p) for p in proofs]
     if not texts:
         return []
+    n = len(texts)
+    res = np.empty(n, dtype=np.int8)
+    # one pass against the circuit itself; only proofs whose lengths differ (E_SHAPE) are
+    # re-read for their shape and packed again against that shape variant
+    codes = np.empty(n, dtype=np.int32)
+    packed = vkey.pack_many(texts, codes=codes)
     groups = {}
-    for i, t in enumerate(texts):
-        groups.setdefault(id(vk := vkey.for_proof(t)), (vk, []))[1].append(i)
-    res = np.empty(len(texts), dtype=np.int8)
+    for i in np.flatnonzero(codes != E_OK):
+        if codes[i] != E_SHAPE:
+            raise P2VError(int(codes[i]), f"proof {i}: " + _pack_error(vkey, texts[i]))
+        try:
+            vk = vkey.for_proof(texts[i])
+        except P2VError:
+            # lengths past this build's limits (include/p2v.h, 2^20): the transcript cannot match
+            # the circuit's, so the reference's answer is False (barring a PoW collision)
+            res[i] = REJECT
+            continue
+        if vk is vkey:   # another list-length mismatch: an `error` in the reference as well
+            raise P2VError(E_SHAPE, f"proof {i}: " + _pack_error(vkey, texts[i]))
+        groups.setdefault(id(vk), (vk, []))[1].append(int(i))
+    good = np.flatnonzero(codes == E_OK)
+    if good.size:
+        sub = np.empty(good.size, dtype=np.int8)
+        rows = np.ascontiguousarray(packed[good])
+        _check(lib().p2v_verify_batch(vkey.handle, rows.ctypes.data, good.size, sub.ctypes.data, device))
+        res[good] = sub
     for vk, idx in groups.values():
-        packed = vk.pack_many([texts[i] for i in idx])
+        rows = vk.pack_many([texts[i] for i in idx])
         sub = np.empty(len(idx), dtype=np.int8)
-        _check(lib().p2v_verify_batch(vk.handle, packed.ctypes.data, len(idx), sub.ctypes.data, device))
+        _check(lib().p2v_verify_batch(vk.handle, rows.ctypes.data, len(idx), sub.ctypes.data, device))
         res[idx] = sub
     out: List[Union[bool, VerifierError]] = []
     for st in res:

@@ -286,35 +286,42 @@ def test_gpu_chained_workspaces(p2v):
     assert np.array_equal(bvs[1].run(batches[3]), want[3])
 
 
-@pytest.mark.parametrize("B,tiled", [(200, False), (2048, True)])
-def test_gpu_transcript_lookahead(p2v, B, tiled):
+@pytest.mark.parametrize("B,tiled,mixed", [(200, False, False), (2048, True, False), (1, False, True), (64, True, True)])
+def test_gpu_transcript_lookahead(p2v, B, tiled, mixed):
     """P2V_FLAG_LOOKAHEAD: each batch's transcript runs on the workspace's own transcript stream
     into one of two challenge buffers, ahead of the workspace's earlier batches.  Two workspaces,
     12 different batches (rotations of a pool with valid and corrupted proofs) in flight without
     host syncs, each workspace reused every other batch (both challenge buffers cycle): every
-    batch's statuses equal a plain synchronous run's.  B = 2048 runs the quad transcript and the
-    tiled layout, B = 200 the row transcript."""
+    batch's statuses and full traces equal a plain synchronous run's.  B = 2048 runs the quad
+    transcript and the tiled layout, B = 200 the row transcript; B = 1 and 64 are latency mode
+    (k_fri and the coset / misc vanishing kernels on streams of their own, waiting on the
+    lookahead's events), with lookahead and plain runs interleaved on each workspace (mixed;
+    ADVICE r3)."""
     import torch
     gc = gen_circuit(6, 4, 0, 1, 28, 16, 0, 1)
     vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
     pool = [gc.proof(1, 1), gc.proof(2, 2), gc.proof(1, 3, flags=1), gc.proof(1, 4, flags=4), gc.proof(2, 5, flags=2)]
     packed = vk.pack_many(pool)
     nb = 12
+    tw = vk.info.trace_words
     batches = [np.ascontiguousarray(packed[(np.arange(B) * (k + 1) + k) % len(pool)]) for k in range(nb)]
     ref = p2v.BatchVerifier(vk, 0, B)
-    want = [ref.run(b) for b in batches]
+    want = [ref.run(b, trace=True) for b in batches]
     bvs = [p2v.BatchVerifier(vk, 0, B) for _ in range(2)]
     streams = [torch.cuda.Stream() for _ in range(2)]
     d_in = [torch.from_numpy((p2v.tile_proofs(b) if tiled else b).view(np.int64)).cuda() for b in batches]
     d_res = [torch.full((B,), 7, dtype=torch.int8, device="cuda") for _ in batches]
+    d_tr = [torch.zeros((B, tw), dtype=torch.int64, device="cuda") for _ in batches]
     torch.cuda.synchronize()
     for k in range(nb):
+        la = (k % 3 != 2) if mixed else True
         bvs[k % 2].run_device(d_in[k].data_ptr(), B, d_res[k].data_ptr(), stream=streams[k % 2].cuda_stream, sync=False,
-                              tiled=tiled, lookahead=True)
+                              tiled=tiled, lookahead=la, trace_ptr=d_tr[k].data_ptr())
     torch.cuda.synchronize()
     for k in range(nb):
-        assert np.array_equal(d_res[k].cpu().numpy(), want[k]), k
-    assert {1, -3, 0} <= set(np.concatenate(want).tolist())
+        assert np.array_equal(d_res[k].cpu().numpy(), want[k][0]), k
+        assert np.array_equal(d_tr[k].cpu().numpy().view(np.uint64), want[k][1]), k
+    assert {1, -3, 0} <= set(np.concatenate([w[0] for w in want]).tolist()) or B == 1
 
 
 def _number_paths(d, path=()):
@@ -674,6 +681,24 @@ def test_gpu_shape_variants_vs_oracle(p2v, mode, ext):
         res, tr = p2v.BatchVerifier(v, 0, 1).run(v.pack(pj)[None, :], trace=True)
         st, otr = O.verify_json(gc.common, gc.vkey, pj, trace=True)
         assert int(res[0]) == st and np.array_equal(tr[0], otr), name
+
+
+def test_gpu_batch_shape_past_the_limit_is_false(p2v):
+    """verify_proof_batch: a proof whose public-input list is longer than this
+    build's shape-variant limit (2^20) is False — its transcript cannot match, as in the
+    reference, which hashes the list at any length — while the rest of the batch is verified
+    as usual; a proof that does not decode still raises, as aeson's decode fails."""
+    gc = gen_circuit(6, 4, 0, 1, 28, 16, 0, 1)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    good, bad3 = gc.proof(1, 1), gc.proof(1, 4, flags=1)
+    d = json.loads(good)
+    d["public_inputs"] = [0] * ((1 << 20) + 1)
+    long_pi = json.dumps(d, separators=(",", ":")).encode()
+    got = p2v.verify_proof_batch(vk, [good, long_pi, bad3, good])
+    assert got[0] is True and got[1] is False and got[3] is True, got
+    assert isinstance(got[2], p2v.VerifierError) and got[2].status == -3, got
+    with pytest.raises(p2v.P2VError):
+        p2v.verify_proof_batch(vk, [good, b"{"])
 
 
 def test_gpu_c5_shard_one_launch(p2v):
