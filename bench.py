@@ -392,18 +392,20 @@ def max_over_ranks(dt, world, cpu_grp):
     return float(t.item())
 
 
-def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, cpu_grp, streams, tiled, steps=1, stagger=0):
+def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, cpu_grp, streams, tiled, steps=1, stagger=0,
+           total=C5_PROOFS, chunk=C5_CHUNK, note=None):
     """BASELINE.json configs[4] (C5): 1 048 576 std proofs sharded over the ranks (contiguous
     shards, p2v.shard_bounds), each rank verifying its shard in launches of up to 131 072 proofs
     (the per-GPU share at 8 GPUs) on two workspaces in flight.  The shard is device-resident:
     the C2 batch repeated on the device to 131 072 distinct HBM rows, reused by every launch of
     the shard.  Statuses of every launch are checked: the result buffers are cleared before the
     timed pass and each launch's statuses are compared with the expected vector on its own
-    stream, folded into a per-stream device flag.  Time = max over ranks."""
+    stream, folded into a per-stream device flag.  Time = max over ranks.
+    total / chunk / note: the same leg for another configuration (C3: 65 536 lookup proofs)."""
     import torch
-    s, e = p2v.shard_bounds(C5_PROOFS, world, int(os.environ.get("RANK", "0")))
+    s, e = p2v.shard_bounds(total, world, int(os.environ.get("RANK", "0")))
     n = e - s
-    rows = min(C5_CHUNK, n)
+    rows = min(chunk, n)
     reps = (rows + B - 1) // B
     if tiled:   # whole 64-proof tiles of the tiled batch, repeated (proof order is preserved)
         big = d_proofs.repeat(reps)[: (rows + 63) // 64 * 64 * info.proof_words].contiguous()
@@ -445,12 +447,52 @@ def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, cpu_grp, str
     dt = max_over_ranks(dt, world, cpu_grp)
     del big, bvs, res
     torch.cuda.empty_cache()
-    return {"proofs": C5_PROOFS * steps, "value": round(C5_PROOFS * steps / dt, 1), "unit": "proofs/s",
-            "per_gpu": round(C5_PROOFS * steps / dt / world, 1), "seconds": round(dt, 4), "n_gpus": world,
+    return {"proofs": total * steps, "value": round(total * steps / dt, 1), "unit": "proofs/s",
+            "per_gpu": round(total * steps / dt / world, 1), "seconds": round(dt, 4), "n_gpus": world,
             "shard_per_gpu": n, "launch_proofs": rows, "verified_all": ok,
-            "note": "BASELINE configs[4]: 1M std proofs sharded over the ranks (no data-path collective), "
-                    "launches of <= 131072 device-resident proofs, two in flight per GPU, every launch's statuses checked on "
-                    "the device; time = max over ranks"}
+            "note": note or ("BASELINE configs[4]: 1M std proofs sharded over the ranks (no data-path collective), "
+                             "launches of <= 131072 device-resident proofs, two in flight per GPU, every launch's statuses checked on "
+                             "the device; time = max over ranks")}
+
+
+C3_PROOFS = 65536   # BASELINE.json configs[2]
+C3_CHUNK = 16384
+
+
+def c3_leg(p2v, args, threads, dev, local, streams):
+    """BASELINE.json configs[2] (C3): 65 536 proofs of the real circuit with LookupGate /
+    LookupTableGate blocks and a live lookup argument (a 256-entry and a 2^16-entry table,
+    Plonk/Lookups.hs:45-132), on one GPU: 64 distinct generated proofs, 1/16 corrupted, tiled
+    and repeated on the device to 65 536 rows, verified in launches of 16 384 on two workspaces
+    in flight, every launch's statuses checked on the device.  Per-kernel times (k_lut and the
+    vanishing kernels, which include the lookup items) from one serial 4 096-proof run."""
+    import torch
+    t0 = time.time()
+    gc, proofs = make_workload(args.degree_bits, args.distinct, args.witnesses, 7, threads, 2, True)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    info = vk.info
+    rows = np.ascontiguousarray(vk.pack_many(proofs)[np.arange(args.batch) % len(proofs)])
+    expect = mutate_batch(rows, info)
+    d_proofs = torch.from_numpy(p2v.tile_proofs(rows).view(np.int64)).to(dev)
+    d_expect = torch.from_numpy(expect).to(dev)
+    gen_s = time.time() - t0
+    out = c5_leg(p2v, vk, info, d_proofs, d_expect, args.batch, 1, local, dev, None, streams, True,
+                 total=C3_PROOFS, chunk=C3_CHUNK,
+                 note="BASELINE configs[2]: 65536 proofs of the real circuit with LookupGate/LookupTableGate (256 + 65536-entry "
+                      "tables, live lookup argument), device-resident, launches of 16384, two in flight, statuses checked on the device")
+    bv = p2v.BatchVerifier(vk, local, args.batch)
+    res = torch.empty(args.batch, dtype=torch.int8, device=dev)
+    kt = {}
+    for _ in range(3):   # serial 4096-proof runs: per-kernel times of the lookup circuit
+        bv.run_device(d_proofs.data_ptr(), args.batch, res.data_ptr(), stream=streams[0].cuda_stream, sync=True, tiled=True)
+        for k, v in bv.last_timings().items():
+            kt.setdefault(k, []).append(v)
+    out["verified_all"] = out["verified_all"] and bool((res == d_expect).all())
+    out["kernel_ms_serial_4096"] = {k: round(float(np.mean(v[1:])), 4) for k, v in kt.items()}
+    out["workload"] = f"{len(proofs)} distinct proofs generated in {gen_s:.1f}s, degree_bits {info.degree_bits}, {info.proof_words} words per proof"
+    del d_proofs, bv
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -483,6 +525,7 @@ def main():
                     help="nccl (= RCCL; the driver's multi-GPU runs) or gloo (rehearsing N ranks on fewer GPUs)")
     ap.add_argument("--quick", action="store_true", help="device-resident figure only (no ingest / PCIe / CPU / C5 legs)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 leg (1M proofs sharded over the ranks)")
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 leg (65536 lookup-circuit proofs, one GPU)")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -630,6 +673,9 @@ def main():
     if not args.quick and not args.no_c5:
         c5 = c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, cpu_grp, streams, lay_tiled,
                     stagger=args.stagger)
+    c3 = None
+    if world == 1 and not args.quick and not args.no_c3 and not args.lookups and real:
+        c3 = c3_leg(p2v, args, threads, dev, local, streams)
     if rank == 0:
         kb = kernel_bytes_model(info, info.trace_words)
         # dominant kernel: the longest launch on the main stream (k_transcript / k_vanish / k_fri /
@@ -688,6 +734,8 @@ def main():
             out["roofline"]["valu_issue_frac"] = out["valu"]["issue"]["step_frac"]
         if c5 is not None:
             out["c5"] = c5
+        if c3 is not None:
+            out["c3"] = c3
         if world == 1 and not args.quick:
             out["ingest"] = ingest_rate(vk, proofs, threads)
             out["h2d_end_to_end"] = h2d_rate(bvs, rows, B, expect)
