@@ -61,6 +61,8 @@ def pmc_tag():
     tags = []
     for f in glob.glob(os.path.join(ROOT, "profiles", "*_pmc_valu.json")):
         tag = os.path.basename(f)[: -len("_pmc_valu.json")]
+        if tag.endswith("_c3"):   # the C3 circuit's passes (profile_round.sh step 5) are not the line's workload
+            continue
         if os.path.exists(os.path.join(ROOT, "profiles", f"{tag}_pmc_traffic.json")):
             tags.append(tag)
     return max(tags) if tags else None

@@ -38,20 +38,32 @@ def main():
         p = os.path.join(src, name)
         if os.path.exists(p):
             shutil.copy(p, os.path.join(prof, f"{tag}_{name}"))
-    fetch = per_kernel(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    out = traffic_summary(src, "", tag, prof)
+    vpath = os.path.join(src, "pmc_valu", "run_counter_collection.csv")
+    if os.path.exists(vpath):
+        valu_summary(vpath, tag, prof)
+    print(json.dumps({k: v for k, v in out.items() if not k.endswith("_KiB")}, indent=1))
+    # the C3 circuit's passes (profile_round.sh step 5), when present: <tag>_c3_*
+    if os.path.exists(os.path.join(src, "c3_pmc_fetch")):
+        shutil.copy(os.path.join(src, "c3_trace_serial", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_c3_kernel_stats_serial.csv"))
+        traffic_summary(src, "c3_", tag + "_c3", prof)
+        valu_summary(os.path.join(src, "c3_pmc_valu", "run_counter_collection.csv"), tag + "_c3", prof)
+
+
+def traffic_summary(src, pre, tag, prof):
+    """<tag>_pmc_traffic.json from the <pre>pmc_fetch / <pre>pmc_write passes."""
+    fetch = per_kernel(os.path.join(src, pre + "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(src, pre + "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     out = {"_note": "HBM bytes per launch (median over launches) from rocprofv3 PMC, separate FETCH_SIZE / WRITE_SIZE "
                     "passes of bench.py --steps 3 --inflight 1, corrected per MI355X_MICROARCH.md HBM section: "
-                    "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024; batch = 4096 std proofs; round " + tag}
+                    "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024; batch = 4096 "
+                    + ("C3 (live lookup) proofs" if pre else "std proofs") + "; round " + tag}
     for k in sorted(set(fetch) | set(write)):
         f, w = fetch.get(k, 0.0), write.get(k, 0.0)
         out[k] = int(round((2 * f + w) * 1024))
         out[k + "_raw_KiB"] = {"FETCH_SIZE": f, "WRITE_SIZE": w}
     json.dump(out, open(os.path.join(prof, f"{tag}_pmc_traffic.json"), "w"), indent=1)
-    vpath = os.path.join(src, "pmc_valu", "run_counter_collection.csv")
-    if os.path.exists(vpath):
-        valu_summary(vpath, tag, prof)
-    print(json.dumps({k: v for k, v in out.items() if not k.endswith("_KiB")}, indent=1))
+    return out
 
 
 VALU_COUNTERS = ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU2", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_WAVES",
