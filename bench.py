@@ -522,6 +522,10 @@ def main():
     ap.add_argument("--arities", default="", help="comma-separated FRI arity bits (with --ext 1: MinSize; else Fixed)")
     ap.add_argument("--lookups", type=int, default=0,
                     help="0: standard recursion circuit (C2); 2: + LookupGate/LookupTableGate with a 256-entry and a 2^16-entry table (C3 circuit)")
+    ap.add_argument("--transcript", choices=("auto", "row", "quad", "pair", "lane"), default="auto",
+                    help="transcript layout (P2V_TRANSCRIPT): auto = row below 2048 proofs, quad from 2048 on")
+    ap.add_argument("--single-stream", action="store_true", help="P2V_SINGLE_STREAM=1: each workspace on one stream (no side stream)")
+    ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES for this process (0: the runtime's default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL; the driver's multi-GPU runs) or gloo (rehearsing N ranks on fewer GPUs)")
@@ -551,6 +555,14 @@ def main():
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # read by libp2v when a workspace is created / by the HIP runtimes at initialisation: set
+    # before anything touches the GPU
+    if args.transcript != "auto":
+        os.environ["P2V_TRANSCRIPT"] = args.transcript
+    if args.single_stream:
+        os.environ["P2V_SINGLE_STREAM"] = "1"
+    if args.hw_queues:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -711,7 +723,10 @@ def main():
                                    f"{' in 64-proof tiles' if lay_tiled else ' proof-major'}",
                        "global_batch": B * world, "degree_bits": info.degree_bits, "parallelism": f"proof-sharded x{world}",
                        **({"ext": args.ext} if args.ext else {}),
-                       "inflight": nv, "stagger": bool(args.stagger and nv > 1), "lookahead": bool(args.lookahead)},
+                       "inflight": nv, "stagger": bool(args.stagger and nv > 1), "lookahead": bool(args.lookahead),
+                       **({"transcript": args.transcript} if args.transcript != "auto" else {}),
+                       **({"single_stream": True} if args.single_stream else {}),
+                       **({"hw_queues": args.hw_queues} if args.hw_queues else {})},
             "clock": {**clock, "note": "the timed pass on the device clock: HIP events on each workspace stream (start before its "
                                        "first launch, one after every launch); step_ms = intervals between successive completions"},
             "serial": {"value": round(total / dt_serial, 1), "ms_per_step": round(dt_serial / args.steps * 1e3, 4),

@@ -22,6 +22,8 @@
 
 extern "C" __global__ void k_transpose(const uint64_t*, int64_t, int, uint64_t*, int);
 extern "C" __global__ void k_phase1(DevCircuit, int, int);
+extern "C" __global__ void k_phase1_lane(DevCircuit, int, int);
+extern "C" __global__ void k_phase1_pair(DevCircuit, int, int);
 extern "C" __global__ void k_transcript(DevCircuit, int);
 extern "C" __global__ void k_transcript_x(DevCircuit, int);
 extern "C" __global__ void k_leaf(DevCircuit);
@@ -135,7 +137,7 @@ struct p2v_verifier {
   float last_ms[kNumKernels] = {0};
   bool timed = false;
   bool fri_first = false;           // side stream order: k_fri before the vanishing kernels (env P2V_FRI_FIRST=1)
-  int transcript_mode = 0;          // 0 auto, 1 row, 2 quad (env P2V_TRANSCRIPT)
+  int transcript_mode = 0;          // 0 auto, 1 row, 2 quad, 3 lane, 4 pair (env P2V_TRANSCRIPT)
   int quad_min_batch = 2048;        // auto: quad form from this batch size on
   bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
   int side_prio = 0;                // env P2V_SIDE_PRIO=1: side stream at the device's highest priority (measured: no effect)
@@ -398,7 +400,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (const char* f1 = getenv("P2V_PHASE1")) v->split_phase1 = !strcmp(f1, "split") ? 1 : !strcmp(f1, "excl") ? 2 : 0;
   if (const char* ff = getenv("P2V_FRI_FIRST")) v->fri_first = ff[0] == '1';
   if (const char* sw = getenv("P2V_SIDE_WG")) v->side_wg = atoi(sw) == 64 ? 64 : 256;
-  if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : 0;
+  if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : !strcmp(tm, "lane") ? 3 : !strcmp(tm, "pair") ? 4 : 0;
   DevCircuit& d = v->dc;
   memset(&d, 0, sizeof d);
   d.r = C.r; d.Q = C.num_queries; d.S = (int)C.arities.size(); d.T = 4 + d.S;
@@ -654,6 +656,8 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   int tl = d.B >= v->quad_min_batch ? 4 : 16;
   if (v->transcript_mode == 1) tl = 16;
   else if (v->transcript_mode == 2) tl = 4;
+  else if (v->transcript_mode == 3) tl = 1;
+  else if (v->transcript_mode == 4) tl = 2;
   const int nt_blocks = (tl * d.B + 255) / 256;
   const int leaf_units = d.Q * d.T * NPB;
   // staggered workspaces (p2v_verifier_chain): phase 1 after the linked workspace's latest one
@@ -687,7 +691,9 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));
   } else if (!v->split_phase1 || sd == st) {
     T0(1, st);
-    k_phase1<<<nt_blocks + (leaf_units + 3) / 4, 256, 0, st>>>(d, nt_blocks, tl);
+    if (tl == 1) k_phase1_lane<<<nt_blocks + (leaf_units + 3) / 4, 256, 0, st>>>(d, nt_blocks, tl);
+    else if (tl == 2) k_phase1_pair<<<nt_blocks + (leaf_units + 3) / 4, 256, 0, st>>>(d, nt_blocks, tl);
+    else k_phase1<<<nt_blocks + (leaf_units + 3) / 4, 256, 0, st>>>(d, nt_blocks, tl);
     DBG("k_phase1", st);
     T1(1, st);
     if (sd != st) {

@@ -68,6 +68,9 @@ GL_HD uint64_t reduce96_nc(uint64_t hi, uint64_t lo) {
   return r;
 }
 
+#ifndef P2V_MUL_CMAD
+#define P2V_MUL_CMAD 1   // the product's carry-free MADs in plain C (no inline-asm SGPR outputs)
+#endif
 #ifndef P2V_MUL_PRODUCT
 #define P2V_MUL_PRODUCT 1   // device multiply's partial products: 1 = chained MAD addends (round 4), 0 = carry adds
 #endif
@@ -106,7 +109,7 @@ __device__ __forceinline__ uint32_t mask_1(uint64_t m) { uint32_t d; asm("v_cndm
 //          (12 VALU when not taken): the Poseidon S-box (p2::mul_nc);
 //   V = 0: one fix-up per wrap (16 VALU), the first form, kept for measurement.
 template <int V = 1>
-__device__ __forceinline__ uint64_t mul_nc_dev_v(uint64_t a, uint64_t b) {
+__device__ __forceinline__ uint64_t mul_nc_dev_v(uint64_t a, uint64_t b, uint64_t& negm) {
   using namespace ax;
   const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
   uint64_t cm, c1, c2, ct, c4, bw1, bw2, bw3, bw4;
@@ -119,10 +122,19 @@ __device__ __forceinline__ uint64_t mul_nc_dev_v(uint64_t a, uint64_t b) {
   // product = lo(a0 b0) + lo(y) 2^32 + h 2^64 + cm 2^96: 4 MADs and 2 zero-extensions against
   // 4 MADs and 3 carry adds (round 4)
   (void)c1; (void)c2;
+#if P2V_MUL_CMAD
+  // the MADs whose carry-out is not needed in plain C: the compiler emits the same
+  // v_mad_u64_u32 and, unlike after an inline-asm SGPR output, knows no wait state is needed
+  const uint64_t p00 = (uint64_t)a0 * b0;
+  const uint64_t x = (uint64_t)a0 * b1 + (p00 >> 32);
+  const uint64_t y = mad_co(a1, b0, x, cm);
+  const uint64_t hh = (uint64_t)a1 * b1 + (y >> 32);
+#else
   const uint64_t p00 = mad0(a0, b0);
   const uint64_t x = mad_nc(a0, b1, p00 >> 32);
   const uint64_t y = mad_co(a1, b0, x, cm);
   const uint64_t hh = mad_nc(a1, b1, y >> 32);
+#endif
   const uint32_t h0 = (uint32_t)hh, h1 = (uint32_t)(hh >> 32);          // + cm: below
   const uint64_t lo = ((uint64_t)(uint32_t)y << 32) | (uint32_t)p00;
 #else
@@ -135,15 +147,17 @@ __device__ __forceinline__ uint64_t mul_nc_dev_v(uint64_t a, uint64_t b) {
   const uint32_t h1 = addc0((uint32_t)(p11 >> 32), c2);                 // + cm: below
   const uint64_t lo = ((uint64_t)lo1 << 32) | (uint32_t)p00;
 #endif
-  if constexpr (V == 2) {
+  if constexpr (V == 2 || V == 3) {
   // as below, but the -2^64 case (only when the product has bits 64..95 zero and bits 0..63
-  // below 2^32, e.g. powers of two) is a wave-uniform branch that is almost never taken
+  // below 2^32, e.g. powers of two) is a wave-uniform branch that is almost never taken.
+  // V = 3: no branch here; the caller receives the lanes that still need it (mul_nc_part)
   (void)c4; (void)bw3; (void)bw4;
   const uint64_t t = madm1_co(h0, lo, ct);
   const uint32_t ul = subb_co((uint32_t)t, h1, cm, bw1);
   const uint32_t uh = subb0_co((uint32_t)(t >> 32), bw1, bw2);
   const uint64_t pos = ct & ~bw2, neg = bw2 & ~ct;
   uint64_t r = madm1_co(mask_1(pos), ((uint64_t)uh << 32) | ul, c4);
+  if constexpr (V == 3) { negm = neg; return r; }
   if (__builtin_expect(neg != 0, 0)) r = add64(r, ((uint64_t)mask_m1(neg) << 32) | sel(0u, 1u, neg));
   return r;
   } else if constexpr (V == 1) {
@@ -168,6 +182,16 @@ __device__ __forceinline__ uint64_t mul_nc_dev_v(uint64_t a, uint64_t b) {
   const uint32_t rh2 = subb0_co(rh, bw3, bw4);
   return ((uint64_t)rh2 << 32) | rl2;
   }
+}
+template <int V = 1>
+__device__ __forceinline__ uint64_t mul_nc_dev_v(uint64_t a, uint64_t b) { uint64_t n; return mul_nc_dev_v<V>(a, b, n); }
+// the S-box form without its rare branch: r, and in `neg` the lanes whose product wrapped below
+// 0 (r is then 2^64 too small); mul_fix_neg adds it back (+2^64 == +(2^32 - 1) mod p, as
+// 2^64 - 2^32 + 1 mod 2^64).  A caller merges the branches of independent products into one.
+__device__ __forceinline__ uint64_t mul_nc_part(uint64_t a, uint64_t b, uint64_t& neg) { return mul_nc_dev_v<3>(a, b, neg); }
+__device__ __forceinline__ uint64_t mul_fix_neg(uint64_t r, uint64_t neg) {
+  using namespace ax;
+  return add64(r, ((uint64_t)mask_m1(neg) << 32) | sel(0u, 1u, neg));
 }
 // the general-purpose multiply (FRI, vanishing, gates): the branch-free one-fix-up form.  (The
 // round-1 build option that put the branch form V = 2 here is gone: it was slower, and the one

@@ -19,6 +19,7 @@
 #include "devcommon.h"
 #include "qposeidon.h"
 #include "rposeidon.h"
+#include "pposeidon.h"
 
 using namespace p2d;
 using gl::E;
@@ -247,7 +248,7 @@ __device__ __forceinline__ void transcript_quad(const DevCircuit& c, int p, int 
           const int pos = 3 * t + j, w = k + pos - start;
           mine[j] = pos >= start && pos < start + take;
           v[j] = 0;
-          if (type == TOP_ABSORB_SOA) { if (mine[j]) v[j] = ld(c, (int64_t)a + w, p); }
+          if (type == TOP_ABSORB_SOA) { const uint64_t u = ld(c, (int64_t)a + (mine[j] ? w : 0), p); v[j] = mine[j] ? u : 0; }
           else if (type == TOP_ABSORB_PIH) { const int q = w & 3; v[j] = q == 0 ? pih[0] : q == 1 ? pih[1] : q == 2 ? pih[2] : pih[3]; }
           else v[j] = c.digest[w & 3];
         }
@@ -291,10 +292,181 @@ __device__ __forceinline__ void transcript_quad(const DevCircuit& c, int p, int 
   }
 }
 
-// one workgroup of transcripts: `tl` lanes per proof (16: row form, 4: quad form)
-__device__ __forceinline__ void transcript_block(const DevCircuit& c, int tl, const qp::TLds& T) {
+// Lane form of the same transcript: one lane per proof, the whole state in its registers, the
+// throughput permutation (p2::permute_dev).  A third of the quad form's VALU instructions per
+// proof, but a chain ~3.5x longer (a lone wave issues its dependent permutation at its own
+// latency): for pipelines with enough batches in flight to hide it (round 4, P2V_TRANSCRIPT=lane).
+__device__ __forceinline__ void transcript_lane(const DevCircuit& c, int p) {
+  uint64_t x[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) x[i] = 0;
+  for (int i = 0; i < c.num_pis; i += 8) {   // public inputs hash, Hash/Sponge.hs:26-31
+    const int k = c.num_pis - i;
+#pragma unroll
+    for (int j = 0; j < 8; j++) if (j < k) x[j] = ld(c, c.pis + i + j, p);
+    p2::permute_dev(x);
+  }
+  uint64_t pih[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) { pih[w] = x[w]; chal(c, CH_PI(c) + w, p) = pih[w]; }
+#pragma unroll
+  for (int i = 0; i < 12; i++) x[i] = 0;
+  int nbuf = 0, outpos = -1;
+  bool absorbing = true;
+  const uint64_t qmask = (1ULL << c.lde_bits) - 1;
+  uint64_t fa0 = 0, fa1 = 0;
+  for (int o = 0; o < c.ntops; o++) {
+    const int type = c.tops[3 * o], a = c.tops[3 * o + 1], n = c.tops[3 * o + 2];
+    if (type == TOP_COPY) { for (int k = 0; k < n; k++) chal(c, a + k, p) = chal(c, a - 3 * c.r + k, p); continue; }
+    if (type == TOP_ZERO) { for (int k = 0; k < n; k++) chal(c, a + k, p) = 0; continue; }
+    if (type <= TOP_ABSORB_DIGEST) {   // absorb n words, chunk by chunk (lazy duplex, Challenge/Pure.hs:38-69)
+      if (!absorbing) { absorbing = true; nbuf = 0; }
+      for (int k = 0; k < n;) {
+        const int start = nbuf == 8 ? 0 : nbuf;
+        const int take = (8 - start) < (n - k) ? (8 - start) : (n - k);
+        if (nbuf == 8) { p2::permute_dev(x); nbuf = 0; }   // overwrite mode: the rate part is replaced
+#pragma unroll
+        for (int j = 0; j < 8; j++) {   // (loaded after the permutation: no registers held across it)
+          const int w = k + j - start;
+          if (j < start || j >= start + take) continue;
+          if (type == TOP_ABSORB_SOA) x[j] = ld(c, (int64_t)a + w, p);
+          else if (type == TOP_ABSORB_PIH) { const int q = w & 3; x[j] = q == 0 ? pih[0] : q == 1 ? pih[1] : q == 2 ? pih[2] : pih[3]; }
+          else x[j] = c.digest[w & 3];
+        }
+        nbuf += take;
+        k += take;
+      }
+      continue;
+    }
+    for (int k = 0; k < n; k++) {   // squeeze: output order state[7], state[6], ...
+      if (absorbing || outpos < 0) { p2::permute_dev(x); absorbing = false; outpos = 7; }
+      uint64_t w;
+      switch (outpos) {   // uniform: a switch, not a dynamically indexed (scratch) array
+        case 0: w = x[0]; break;
+        case 1: w = x[1]; break;
+        case 2: w = x[2]; break;
+        case 3: w = x[3]; break;
+        case 4: w = x[4]; break;
+        case 5: w = x[5]; break;
+        case 6: w = x[6]; break;
+        default: w = x[7]; break;
+      }
+      outpos--;
+      if (type == TOP_SQUEEZE_IDX) w &= qmask;
+      if (a + k == CH_FRI_ALPHA(c)) fa0 = w;
+      if (a + k == CH_FRI_ALPHA(c) + 1) fa1 = w;
+      chal(c, a + k, p) = w;
+    }
+  }
+  // precomputeReducedOpenings, Plonk/FRI.hs:128-134: Y = sum alpha^i y_i, Horner from the top
+  const E alpha{fa0, fa1};
+#pragma unroll
+  for (int b = 0; b < 2; b++) {
+    const int64_t n = b == 0 ? c.n_this : c.n_next, off = b == 0 ? c.o_const : c.o_zs_next;
+    const E y = horner_strided<1>(c, off, n, 0, p, alpha);
+    chal(c, (b == 0 ? CH_Y0(c) : CH_Y1(c)), p) = y.a;
+    chal(c, (b == 0 ? CH_Y0(c) : CH_Y1(c)) + 1, p) = y.b;
+  }
+}
+
+// Pair form (pposeidon.h: 2 lanes per proof, 6 state words per lane): about half of the quad's
+// instructions per proof at a shorter chain (round 4)
+__device__ __forceinline__ void transcript_pair(const DevCircuit& c, int p, int t, const pp::TLdsP& T) {
+  uint64_t x[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < c.num_pis; i += 8) {   // public inputs hash, Hash/Sponge.hs:26-31
+    const int k = c.num_pis - i;
+#pragma unroll
+    for (int j = 0; j < 6; j++) {   // selects, not divergent stores: x stays in registers
+      const int pos = 6 * t + j;
+      const bool mine = pos < 8 && pos < k;
+      const uint64_t v = ld(c, c.pis + i + (mine ? pos : 0), p);
+      x[j] = mine ? v : x[j];
+    }
+    pp::permute(x, t, T);
+  }
+  uint64_t pih[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    pih[w] = pp::get_word(x, w);
+    if (t == 0) chal(c, CH_PI(c) + w, p) = pih[w];
+  }
+#pragma unroll
+  for (int j = 0; j < 6; j++) x[j] = 0;
+  int nbuf = 0, outpos = -1;
+  bool absorbing = true;
+  const uint64_t qmask = (1ULL << c.lde_bits) - 1;
+  uint64_t fa0 = 0, fa1 = 0;
+  for (int o = 0; o < c.ntops; o++) {
+    const int type = c.tops[3 * o], a = c.tops[3 * o + 1], n = c.tops[3 * o + 2];
+    if (type == TOP_COPY) { if (t == 0) for (int k = 0; k < n; k++) chal(c, a + k, p) = chal(c, a - 3 * c.r + k, p); continue; }
+    if (type == TOP_ZERO) { if (t == 0) for (int k = 0; k < n; k++) chal(c, a + k, p) = 0; continue; }
+    if (type <= TOP_ABSORB_DIGEST) {   // absorb n words, chunk by chunk (lazy duplex, Challenge/Pure.hs:38-69)
+      if (!absorbing) { absorbing = true; nbuf = 0; }
+      for (int k = 0; k < n;) {
+        const int start = nbuf == 8 ? 0 : nbuf;
+        const int take = (8 - start) < (n - k) ? (8 - start) : (n - k);
+        // lane t owns rate positions 6t .. 6t+5 (lane 1: 6, 7); the chunk's loads before the
+        // permutation so their latency hides under it
+        uint64_t v[6];
+        bool mine[6];
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+          const int pos = 6 * t + j, w = k + pos - start;
+          mine[j] = pos >= start && pos < start + take;
+          v[j] = 0;
+          if (type == TOP_ABSORB_SOA) { const uint64_t u = ld(c, (int64_t)a + (mine[j] ? w : 0), p); v[j] = mine[j] ? u : 0; }
+          else if (type == TOP_ABSORB_PIH) { const int q = w & 3; v[j] = q == 0 ? pih[0] : q == 1 ? pih[1] : q == 2 ? pih[2] : pih[3]; }
+          else v[j] = c.digest[w & 3];
+        }
+        if (nbuf == 8) { pp::permute(x, t, T); nbuf = 0; }   // overwrite mode: the rate part is replaced
+#pragma unroll
+        for (int j = 0; j < 6; j++) x[j] = mine[j] ? v[j] : x[j];
+        nbuf += take;
+        k += take;
+      }
+      continue;
+    }
+    for (int k = 0; k < n; k++) {   // squeeze: output order state[7], state[6], ...
+      if (absorbing || outpos < 0) { pp::permute(x, t, T); absorbing = false; outpos = 7; }
+      uint64_t w = pp::get_word(x, outpos);
+      outpos--;
+      if (type == TOP_SQUEEZE_IDX) w &= qmask;
+      if (a + k == CH_FRI_ALPHA(c)) fa0 = w;
+      if (a + k == CH_FRI_ALPHA(c) + 1) fa1 = w;
+      if (t == 0) chal(c, a + k, p) = w;
+    }
+  }
+  // precomputeReducedOpenings, Plonk/FRI.hs:128-134: lane t sums the terms i = t (mod 2) in
+  // powers of alpha^2, then Y = H_0 + alpha H_1
+  const E alpha{fa0, fa1};
+  const E al2 = gl::emul(alpha, alpha);
+#pragma unroll
+  for (int b = 0; b < 2; b++) {
+    const int64_t n = b == 0 ? c.n_this : c.n_next, off = b == 0 ? c.o_const : c.o_zs_next;
+    const E h = horner_strided<2>(c, off, n, t, p, al2);
+    const E h0{pp::bcast64(h.a, 0), pp::bcast64(h.b, 0)}, h1{pp::bcast64(h.a, 1), pp::bcast64(h.b, 1)};
+    const E y = gl::eadd(h0, gl::emul(alpha, h1));
+    if (t == 0) { chal(c, (b == 0 ? CH_Y0(c) : CH_Y1(c)), p) = y.a; chal(c, (b == 0 ? CH_Y0(c) : CH_Y1(c)) + 1, p) = y.b; }
+  }
+}
+
+// the constant tables of the transcript forms, in LDS (qposeidon.h TLds, pposeidon.h TLdsP)
+union TLdsAny { qp::TLds q; pp::TLdsP p; };
+
+// one workgroup of transcripts: `tl` lanes per proof (16: row form, 4: quad form); FORM 1: the
+// lane form, FORM 2: the pair form (kernels of their own, so that their register demand does
+// not touch the others')
+template <int FORM = 0>
+__device__ __forceinline__ void transcript_block(const DevCircuit& c, int tl, const TLdsAny& U) {
   const int g = blockIdx.x * 256 + threadIdx.x;
-  if (tl == 16) {
+  const qp::TLds& T = U.q;
+  if constexpr (FORM == 1) {
+    (void)tl; (void)T;
+    if (g < c.B) transcript_lane(c, g);
+  } else if constexpr (FORM == 2) {
+    (void)tl;
+    if ((g >> 1) < c.B) transcript_pair(c, g >> 1, g & 1, U.p);
+  } else if (tl == 16) {
     rp::Row R;
     rp::init(R, threadIdx.x);
     if ((g >> 4) < c.B) transcript_row(c, g >> 4, R, T);
@@ -307,18 +479,31 @@ __device__ __forceinline__ void transcript_block(const DevCircuit& c, int tl, co
 // blocks [0, nt_blocks): transcripts, `tl` lanes per proof (16: row form, 4: quad form) at
 // raised wave priority so co-resident leaf waves do not stretch the serial chain; the
 // rest: leaf hashing, 4 units per block.  Transcript blocks come first so they start first.
-extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_phase1(DevCircuit c, int nt_blocks, int tl) {
+template <int FORM>
+__device__ __forceinline__ void phase1_body(const DevCircuit& c, int nt_blocks, int tl) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  __shared__ qp::TLds T;
+  __shared__ TLdsAny T;
   if ((int)blockIdx.x < nt_blocks) {   // block-uniform branch: the whole workgroup fills T
     __builtin_amdgcn_s_setprio(3);
-    qp::tlds_fill(T, threadIdx.x, 256);
-    transcript_block(c, tl, T);
+    if constexpr (FORM == 0) qp::tlds_fill(T.q, threadIdx.x, 256);
+    if constexpr (FORM == 2) pp::tlds_fill(T.p, threadIdx.x, 256);
+    transcript_block<FORM>(c, tl, T);
     return;
   }
   const int unit = ((int)blockIdx.x - nt_blocks) * 4 + wave;
   const int units = c.Q * c.T * (c.B >> 6);
   if (unit < units) leaf_hash_unit(c, unit, lane);
+}
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_phase1(DevCircuit c, int nt_blocks, int tl) {
+  phase1_body<0>(c, nt_blocks, tl);
+}
+// the lane-form transcript (P2V_TRANSCRIPT=lane) with the leaf hashing
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_phase1_lane(DevCircuit c, int nt_blocks, int tl) {
+  phase1_body<1>(c, nt_blocks, tl);
+}
+// the pair-form transcript (P2V_TRANSCRIPT=pair) with the leaf hashing
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_phase1_pair(DevCircuit c, int nt_blocks, int tl) {
+  phase1_body<2>(c, nt_blocks, tl);
 }
 
 // The same two halves as separate launches (env P2V_PHASE1=split, api.cpp): on their own the leaf
@@ -327,8 +512,8 @@ extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_pe
 // 0.94x): the transcript chains then stretch to the leaf kernel's length; kept for measurement.
 extern "C" __global__ void __launch_bounds__(256) k_transcript(DevCircuit c, int tl) {
   __builtin_amdgcn_s_setprio(3);
-  __shared__ qp::TLds T;
-  qp::tlds_fill(T, threadIdx.x, 256);
+  __shared__ TLdsAny T;
+  qp::tlds_fill(T.q, threadIdx.x, 256);
   transcript_block(c, tl, T);
 }
 // k_transcript with SIMDs of its own: the clobbers below make the kernel allocate the whole
@@ -336,8 +521,8 @@ extern "C" __global__ void __launch_bounds__(256) k_transcript(DevCircuit c, int
 // at the single-wave latency (lat.hip) instead of sharing issue with co-resident leaf waves.
 extern "C" __global__ void __launch_bounds__(256) k_transcript_x(DevCircuit c, int tl) {
   asm volatile("" ::: "v255", "a255");
-  __shared__ qp::TLds T;
-  qp::tlds_fill(T, threadIdx.x, 256);
+  __shared__ TLdsAny T;
+  qp::tlds_fill(T.q, threadIdx.x, 256);
   transcript_block(c, tl, T);
 }
 extern "C" __global__ void __launch_bounds__(256) k_leaf(DevCircuit c) {

@@ -377,23 +377,82 @@ __device__ __forceinline__ uint64_t sbox_dev(uint64_t x) {
   return sbox(x);
 #endif
 }
+// N independent S-boxes x -> x^7 in place, their products interleaved: each stage (x^2; x^3 and
+// x^4; x^7) is one basic block of 1-2 N independent multiplies, and the rare -2^64 fix-up of
+// all of them is one wave-uniform branch per stage (the per-multiply branch of p2::mul_nc made
+// every multiply a basic block of its own: 11 dependent instructions the scheduler could not
+// interleave with the next S-box's).  Round 4.
+template <int N>
+__device__ __forceinline__ void sbox_n(uint64_t* x) {
+  uint64_t x2[N], x3[N], x4[N], n2[N], n3[N], n4[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) x2[i] = gl::mul_nc_part(x[i], x[i], n2[i]);
+  uint64_t any = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) any |= n2[i];
+  if (__builtin_expect(any != 0, 0)) {
+#pragma unroll
+    for (int i = 0; i < N; i++) x2[i] = gl::mul_fix_neg(x2[i], n2[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) { x3[i] = gl::mul_nc_part(x[i], x2[i], n3[i]); x4[i] = gl::mul_nc_part(x2[i], x2[i], n4[i]); }
+  any = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) any |= n3[i] | n4[i];
+  if (__builtin_expect(any != 0, 0)) {
+#pragma unroll
+    for (int i = 0; i < N; i++) { x3[i] = gl::mul_fix_neg(x3[i], n3[i]); x4[i] = gl::mul_fix_neg(x4[i], n4[i]); }
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) x[i] = gl::mul_nc_part(x3[i], x4[i], n2[i]);
+  any = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) any |= n2[i];
+  if (__builtin_expect(any != 0, 0)) {
+#pragma unroll
+    for (int i = 0; i < N; i++) x[i] = gl::mul_fix_neg(x[i], n2[i]);
+  }
+}
+#ifndef P2V_SBOX_ILP
+#define P2V_SBOX_ILP 2   // S-boxes per interleaved group in the full rounds (sbox_n); 0: one p2::sbox per word
+#endif
+// the S-boxes of words [I, E) of a full round
+template <int I, int E>
+__device__ __forceinline__ void sbox_range(uint64_t* s) {
+#if P2V_SBOX_ILP > 0
+  if constexpr (I < E) {
+    constexpr int K = (E - I) < P2V_SBOX_ILP ? (E - I) : P2V_SBOX_ILP;
+    sbox_n<K>(s + I);
+    sbox_range<I + K, E>(s);
+  }
+#else
+#pragma unroll
+  for (int i = I; i < E; i++) s[i] = sbox_dev(s[i]);
+#endif
+}
+__device__ __forceinline__ uint64_t sbox_one(uint64_t x) {
+#if P2V_SBOX_ILP > 0
+  sbox_n<1>(&x);
+  return x;
+#else
+  return sbox_dev(x);
+#endif
+}
 // round r: s -> t (s is clobbered by the S-boxes); t = M sbox(s) + rc[r + 1].
 // zh0: round 0 with state words 8..11 entering as 0 (their S-box outputs are constants).
 // g: which groups of 4 output rows are needed (bit k = rows 4k..4k+3); wave-uniform.
 template <bool FULL>
 __device__ __forceinline__ void round_pp(uint64_t* s, uint64_t* t, int r, bool zh0, int g) {
   if (FULL) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) s[i] = sbox_dev(s[i]);
+    sbox_range<0, 8>(s);
     if (zh0) {
 #pragma unroll
       for (int i = 8; i < 12; i++) s[i] = c_zh.z[i - 8];
     } else {
-#pragma unroll
-      for (int i = 8; i < 12; i++) s[i] = sbox_dev(s[i]);
+      sbox_range<8, 12>(s);
     }
   } else {
-    s[0] = sbox_dev(s[0]);
+    s[0] = sbox_one(s[0]);
   }
   const uint64_t* kl = c_rc_split.lo + 12 * (r + 1);
   const uint64_t* kh = c_rc_split.hi + 12 * (r + 1);
@@ -494,22 +553,22 @@ __device__ __forceinline__ void pblock2_group(const uint64_t* s, uint64_t y2, ui
 template <int D>
 __device__ __forceinline__ void pblock(uint64_t* s, uint64_t* t, const PBlock& B) {
   uint64_t y[D + 1];
-  s[0] = sbox_dev(s[0]);   // y1, word 0 of s'
+  s[0] = sbox_one(s[0]);   // y1, word 0 of s'
   {   // chain row 1 (row 0 of M s' + d1): inline MDS entries
     uint64_t al = madk_s<mds_coeff(0, 0)>((uint32_t)s[0], B.dlo[0]);
     uint64_t ah = madk_s<mds_coeff(0, 0)>((uint32_t)(s[0] >> 32), B.dhi[0]);
     mds_acc<0, 1>(s, al, ah);
-    y[2] = sbox_dev(reduce_rows(al, ah));
+    y[2] = sbox_one(reduce_rows(al, ah));
   }
   if constexpr (D >= 3) {   // chain row 2: row sums < 2^16, the branch form of the fix-up
     uint64_t al, ah;
     prow<mds_coeff(0, 0), 0>(s, nullptr, y[2], B.cf[0], B.dlo[1], B.dhi[1], al, ah);
-    y[3] = sbox_dev(reduce_rows(al, ah));
+    y[3] = sbox_one(reduce_rows(al, ah));
   }
   if constexpr (D >= 4) {   // chain row 3: row sums < 2^24
     uint64_t al, ah;
     prow<mds_coeff(0, 0), 1>(s, y + 2, y[3], B.cf[1], B.dlo[2], B.dhi[2], al, ah);
-    y[4] = sbox_dev(reduce_t(al, ah));
+    y[4] = sbox_one(reduce_t(al, ah));
   }
 #if P2V_MDS_BRANCH == 2
   if constexpr (D == 2) {

@@ -205,11 +205,11 @@ def test_gpu_n12_standard_batch_vs_oracle(p2v):
             assert (tr[lanes] == tr[lanes[0]]).all()
 
 
-@pytest.mark.parametrize("form", ["row", "quad"])
+@pytest.mark.parametrize("form", ["row", "quad", "lane", "pair"])
 @pytest.mark.parametrize("nb,mode,lk,pis", [(6, 1, 0, 4), (6, 0, 2, 0), (8, 1, 0, 19)])
 def test_gpu_transcript_forms_vs_oracle(p2v, form, nb, mode, lk, pis):
-    """The two transcript layouts (16 lanes and 4 lanes per proof; api.cpp picks one by batch
-    size, P2V_TRANSCRIPT forces it) give the oracle's challenges and statuses: real and
+    """The four transcript layouts (16, 4, 2 lanes and 1 lane per proof; api.cpp picks the
+    first two by batch size, P2V_TRANSCRIPT forces any) give the oracle's challenges and statuses: real and
     degenerate circuits, lookups, 0 / 4 / 19 public inputs (19: a partial last PI block)."""
     gc = gen_circuit(nb, pis, lk, mode=mode)
     cases = [c[0] for c in _cases(gc)]
