@@ -25,6 +25,8 @@ extern "C" __global__ void k_phase1(DevCircuit, int, int);
 extern "C" __global__ void k_phase1_lane(DevCircuit, int, int);
 extern "C" __global__ void k_phase1_pair(DevCircuit, int, int);
 extern "C" __global__ void k_transcript(DevCircuit, int);
+extern "C" __global__ void k_transcript_lane(DevCircuit, int);
+extern "C" __global__ void k_transcript_pair(DevCircuit, int);
 extern "C" __global__ void k_transcript_x(DevCircuit, int);
 extern "C" __global__ void k_leaf(DevCircuit);
 extern "C" __global__ void k_merkle(DevCircuit);
@@ -678,7 +680,9 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     d.chal = (uint64_t*)(la_slot ? v->chal2.p : v->chal.p);
     HCK(hipStreamWaitEvent(v->ts, v->chal_free[la_slot], 0));
     T0(9, v->ts);
-    k_transcript<<<nt_blocks, 256, 0, v->ts>>>(d, tl);
+    if (tl == 1) k_transcript_lane<<<nt_blocks, 256, 0, v->ts>>>(d, tl);
+    else if (tl == 2) k_transcript_pair<<<nt_blocks, 256, 0, v->ts>>>(d, tl);
+    else k_transcript<<<nt_blocks, 256, 0, v->ts>>>(d, tl);
     DBG("k_transcript", v->ts);
     T1(9, v->ts);
     HCK(hipEventRecord(v->tr_done[la_slot], v->ts));
@@ -704,6 +708,7 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     // the transcripts first, on st, so their waves claim empty SIMDs before the leaf waves land
     HCK(hipEventRecord(v->dep_p1, st));   // the batch is ready on st
     T0(9, st);
+    if (tl <= 2) return fail(P2V_E_ARG, "P2V_PHASE1=excl takes the row or quad transcript only");
     k_transcript_x<<<nt_blocks, 256, 0, st>>>(d, tl);
     DBG("k_transcript_x", st);
     T1(9, st);
@@ -720,7 +725,9 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     HCK(hipEventRecord(v->dep_p1, st));   // the batch is ready on st (H2D, caller's stream order)
     HCK(hipStreamWaitEvent(sd, v->dep_p1, 0));
     T0(9, sd);
-    k_transcript<<<nt_blocks, 256, 0, sd>>>(d, tl);
+    if (tl == 1) k_transcript_lane<<<nt_blocks, 256, 0, sd>>>(d, tl);
+    else if (tl == 2) k_transcript_pair<<<nt_blocks, 256, 0, sd>>>(d, tl);
+    else k_transcript<<<nt_blocks, 256, 0, sd>>>(d, tl);
     DBG("k_transcript", sd);
     T1(9, sd);
     HCK(hipEventRecord(v->dep_tr, sd));

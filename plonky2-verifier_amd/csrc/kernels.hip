@@ -516,6 +516,18 @@ extern "C" __global__ void __launch_bounds__(256) k_transcript(DevCircuit c, int
   qp::tlds_fill(T.q, threadIdx.x, 256);
   transcript_block(c, tl, T);
 }
+// the lane and pair forms on their own (the lookahead / split launches, api.cpp)
+extern "C" __global__ void __launch_bounds__(256) k_transcript_lane(DevCircuit c, int tl) {
+  __builtin_amdgcn_s_setprio(3);
+  __shared__ TLdsAny T;
+  transcript_block<1>(c, tl, T);
+}
+extern "C" __global__ void __launch_bounds__(256) k_transcript_pair(DevCircuit c, int tl) {
+  __builtin_amdgcn_s_setprio(3);
+  __shared__ TLdsAny T;
+  pp::tlds_fill(T.p, threadIdx.x, 256);
+  transcript_block<2>(c, tl, T);
+}
 // k_transcript with SIMDs of its own: the clobbers below make the kernel allocate the whole
 // register file (256 VGPRs + 256 AGPRs), so each transcript wave is alone on its SIMD and issues
 // at the single-wave latency (lat.hip) instead of sharing issue with co-resident leaf waves.

@@ -286,8 +286,9 @@ def test_gpu_chained_workspaces(p2v):
     assert np.array_equal(bvs[1].run(batches[3]), want[3])
 
 
-@pytest.mark.parametrize("B,tiled,mixed", [(200, False, False), (2048, True, False), (1, False, True), (64, True, True)])
-def test_gpu_transcript_lookahead(p2v, B, tiled, mixed):
+@pytest.mark.parametrize("B,tiled,mixed,form", [(200, False, False, None), (2048, True, False, None), (1, False, True, None),
+                                                 (64, True, True, None), (2048, True, True, "lane"), (256, False, True, "pair")])
+def test_gpu_transcript_lookahead(p2v, B, tiled, mixed, form):
     """P2V_FLAG_LOOKAHEAD: each batch's transcript runs on the workspace's own transcript stream
     into one of two challenge buffers, ahead of the workspace's earlier batches.  Two workspaces,
     12 different batches (rotations of a pool with valid and corrupted proofs) in flight without
@@ -296,17 +297,32 @@ def test_gpu_transcript_lookahead(p2v, B, tiled, mixed):
     transcript and the tiled layout, B = 200 the row transcript; B = 1 and 64 are latency mode
     (k_fri and the coset / misc vanishing kernels on streams of their own, waiting on the
     lookahead's events), with lookahead and plain runs interleaved on each workspace (mixed;
-    ADVICE r3)."""
+    ADVICE r3).  form: the lane / pair transcript layouts (P2V_TRANSCRIPT) on the lookahead stream."""
     import torch
     gc = gen_circuit(6, 4, 0, 1, 28, 16, 0, 1)
     vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
     pool = [gc.proof(1, 1), gc.proof(2, 2), gc.proof(1, 3, flags=1), gc.proof(1, 4, flags=4), gc.proof(2, 5, flags=2)]
     packed = vk.pack_many(pool)
     nb = 12
-    tw = vk.info.trace_words
     batches = [np.ascontiguousarray(packed[(np.arange(B) * (k + 1) + k) % len(pool)]) for k in range(nb)]
-    ref = p2v.BatchVerifier(vk, 0, B)
+    ref = p2v.BatchVerifier(vk, 0, B)   # the default layout, synchronous: the expected results
     want = [ref.run(b, trace=True) for b in batches]
+    old = os.environ.get("P2V_TRANSCRIPT")
+    if form:
+        os.environ["P2V_TRANSCRIPT"] = form
+    try:
+        _lookahead_run(p2v, vk, batches, want, B, tiled, mixed)
+    finally:
+        if old is None:
+            os.environ.pop("P2V_TRANSCRIPT", None)
+        else:
+            os.environ["P2V_TRANSCRIPT"] = old
+
+
+def _lookahead_run(p2v, vk, batches, want, B, tiled, mixed):
+    import torch
+    nb = len(batches)
+    tw = vk.info.trace_words
     bvs = [p2v.BatchVerifier(vk, 0, B) for _ in range(2)]
     streams = [torch.cuda.Stream() for _ in range(2)]
     d_in = [torch.from_numpy((p2v.tile_proofs(b) if tiled else b).view(np.int64)).cuda() for b in batches]
