@@ -91,7 +91,13 @@ def valu_roofline(kavg, ms_step, B):
         if kavg.get(k) and B == 4096:   # per-kernel fractions only at the PMC pass's own batch size
             per[k] = round(c * scale / (kavg[k] * 1e-3) / 1e9 / peak, 3)
     tot = sum(cyc.values()) * scale
+    # the clock the chip held in the PMC pass's dispatches (GRBM_GUI_ACTIVE / 8 / time, the
+    # MI355X guide's effective clock; present from round 4's tags on): the issue fraction of the
+    # dominant kernels at that clock, next to the 2.4 GHz-priced one
+    eff = {k: {"clock_ghz": v["effective_clock_ghz"], "issue_frac": v["issue_frac_at_effective_clock"]}
+           for k, v in pm.items() if not k.startswith("_") and v.get("effective_clock_ghz") and (v.get("duration_s") or 0) > 3e-4}
     return {"unit": "G SIMD issue-cycles/s", "peak": peak,
+            "at_effective_clock": eff or None,
             "step_achieved": round(tot / (ms_step * 1e-3) / 1e9, 1),
             "step_frac": round(tot / (ms_step * 1e-3) / 1e9 / peak, 3),
             "kernel_frac_serial": per, "source": os.path.relpath(vfile, ROOT),

@@ -67,7 +67,18 @@ def traffic_summary(src, pre, tag, prof):
 
 
 VALU_COUNTERS = ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU2", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_WAVES",
-                 "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "SQ_BUSY_CYCLES")
+                 "SQ_INSTS_SALU", "SQ_ACTIVE_INST_VALU", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE")
+
+
+def durations(path):
+    """Median dispatch duration (s) per kernel from the PMC csv's timestamps."""
+    vals = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] != "SQ_INSTS_VALU" or not row["Kernel_Name"].startswith("k_"):
+                continue
+            vals.setdefault(row["Kernel_Name"], []).append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
+    return {k: statistics.median(v) for k, v in vals.items()}
 
 
 def valu_summary(vpath, tag, prof):
@@ -83,10 +94,18 @@ def valu_summary(vpath, tag, prof):
                      "proofs; SQ_INSTS_VALU = wave-level VALU instructions, SQ_ACTIVE_INST_VALU2 = quad-cycles in which "
                      "two VALU instructions issued; issue_cycles = 4 * (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2); "
                      "share = fraction of all VALU instructions of one verification step; round " + tag}
+    dur = durations(vpath)
     for k in sorted(valu["SQ_INSTS_VALU"]):
         vout[k] = {c: valu[c].get(k) for c in valu}
         vout[k]["issue_cycles"] = 4 * (valu["SQ_INSTS_VALU"][k] - valu.get("SQ_ACTIVE_INST_VALU2", {}).get(k, 0.0))
         vout[k]["valu_share"] = round(valu["SQ_INSTS_VALU"][k] / tot, 4)
+        g = valu.get("GRBM_GUI_ACTIVE", {}).get(k)
+        if g and dur.get(k):
+            # the guide's effective clock: GRBM_GUI_ACTIVE summed over the 8 XCDs / 8 / wall time
+            # (reads high on dispatches shorter than ~0.3 ms)
+            vout[k]["duration_s"] = dur[k]
+            vout[k]["effective_clock_ghz"] = round(g / 8 / dur[k] / 1e9, 3)
+            vout[k]["issue_frac_at_effective_clock"] = round(vout[k]["issue_cycles"] / (1024 * g / 8), 3)
     json.dump(vout, open(os.path.join(prof, f"{tag}_pmc_valu.json"), "w"), indent=1)
     print(json.dumps({k: v["valu_share"] for k, v in vout.items() if not k.startswith("_")}, indent=1))
 
