@@ -141,6 +141,7 @@ struct p2v_verifier {
   bool fri_first = false;           // side stream order: k_fri before the vanishing kernels (env P2V_FRI_FIRST=1)
   int transcript_mode = 0;          // 0 auto, 1 row, 2 quad, 3 lane, 4 pair (env P2V_TRANSCRIPT)
   int quad_min_batch = 2048;        // auto: quad form from this batch size on
+  int lane_min_batch = 16384;       // auto: lane form from this batch size on (env P2V_LANE_MIN)
   bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
   int side_prio = 0;                // env P2V_SIDE_PRIO=1: side stream at the device's highest priority (measured: no effect)
   int side_wg = 256;                // env P2V_SIDE_WG=64: one-wave groups for k_fri / k_vanish_final on the side stream
@@ -402,6 +403,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (const char* f1 = getenv("P2V_PHASE1")) v->split_phase1 = !strcmp(f1, "split") ? 1 : !strcmp(f1, "excl") ? 2 : 0;
   if (const char* ff = getenv("P2V_FRI_FIRST")) v->fri_first = ff[0] == '1';
   if (const char* sw = getenv("P2V_SIDE_WG")) v->side_wg = atoi(sw) == 64 ? 64 : 256;
+  if (const char* lm = getenv("P2V_LANE_MIN")) v->lane_min_batch = atoi(lm) > 0 ? atoi(lm) : v->lane_min_batch;
   if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : !strcmp(tm, "lane") ? 3 : !strcmp(tm, "pair") ? 4 : 0;
   DevCircuit& d = v->dc;
   memset(&d, 0, sizeof d);
@@ -655,7 +657,10 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   // transcript form: the row form (16 lanes/proof) has the lowest latency, the quad form
   // (4 lanes/proof) the lowest total cost; large batches hide the quad latency behind
   // their leaf hashing.  P2V_TRANSCRIPT=row|quad overrides (measurement).
-  int tl = d.B >= v->quad_min_batch ? 4 : 16;
+  // from lane_min_batch on, the lane form (one lane per proof, ~half of the quad's issue cycles per
+  // proof, a ~5.7 ms chain): the batch's leaf hashing in the same launch outlasts the chain, so it
+  // costs no latency (C5's 131 072-proof launches +2.9 %, C3's 16 384 +1 %)
+  int tl = d.B >= v->lane_min_batch ? 1 : d.B >= v->quad_min_batch ? 4 : 16;
   if (v->transcript_mode == 1) tl = 16;
   else if (v->transcript_mode == 2) tl = 4;
   else if (v->transcript_mode == 3) tl = 1;
