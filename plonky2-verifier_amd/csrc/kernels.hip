@@ -688,6 +688,44 @@ __device__ __forceinline__ E fold_regs(const DevCircuit& c, int s, int64_t off, 
   for (int k = AR - 1; k >= 0; k--) acc = gl::eadd(gl::emul(acc, beta_over_ofs), a[k]);
   return gl::escale(c.inv_arity[s], acc);
 }
+// Arity 16 in two halves, so that only 8 F^2 values are live (k_fri's 96-VGPR budget held all 16
+// with 152 B/lane of scratch).  The DIT's first three stages act on v[0..7] and v[8..15] alone,
+// giving the 8-point transforms E, O (twiddles w^{-2jk}); the last stage is c_k = E_k + w^{-k} O_k,
+// c_{k+8} = E_k - w^{-k} O_k.  With b = beta/ofs:
+//   sum_{k<16} c_k b^k = (1 + b^8) sum_{k<8} E_k b^k + (1 - b^8) sum_{k<8} O_k (w^{-1} b)^k.
+template <int AR>
+__device__ __forceinline__ E dft8_horner(const DevCircuit& c, const uint64_t* tw, int64_t off, int p, E b) {
+  E a[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) a[k] = lde(c, off + 2 * k, p);
+#pragma unroll
+  for (int len = 2; len <= 8; len <<= 1) {
+#pragma unroll
+    for (int i = 0; i < 8; i += len) {
+#pragma unroll
+      for (int k = 0; k < len / 2; k++) {
+        E u = a[i + k], v = a[i + k + len / 2];
+        if (k != 0) v = gl::escale(tw[k * (AR / len)], v);
+        a[i + k] = gl::eadd(u, v);
+        a[i + k + len / 2] = gl::esub(u, v);
+      }
+    }
+  }
+  E acc = gl::e0();
+#pragma unroll
+  for (int k = 7; k >= 0; k--) acc = gl::eadd(gl::emul(acc, b), a[k]);
+  return acc;
+}
+__device__ __forceinline__ E fold16_halves(const DevCircuit& c, int s, int64_t off, int p, E b) {
+  const uint64_t* tw = c.twiddles + 256 * s;
+  const E lo = dft8_horner<16>(c, tw, off, p, b);
+  __builtin_amdgcn_sched_barrier(0);   // keep the halves apart: one half's 8 values live at a time
+  const E hi = dft8_horner<16>(c, tw, off + 16, p, gl::escale(tw[1], b));
+  const E b2 = gl::emul(b, b), b4 = gl::emul(b2, b2), b8 = gl::emul(b4, b4);
+  const E one = gl::eb(1);
+  const E acc = gl::eadd(gl::emul(gl::eadd(one, b8), lo), gl::emul(gl::esub(one, b8), hi));
+  return gl::escale(c.inv_arity[s], acc);
+}
 // generic arity: direct O(arity^2) evaluation of the same interpolant
 __device__ E fold_generic(const DevCircuit& c, int s, int ab, int64_t off, int p, E beta_over_ofs) {
   const int ar = 1 << ab;
@@ -706,6 +744,9 @@ __device__ E fold_generic(const DevCircuit& c, int s, int ab, int64_t off, int p
 
 // k_fri runs on the side stream beside k_merkle (see vanish.hip P2V_SIDE_WAVES): 5 waves per SIMD
 // caps it at 96 VGPRs, so a wave fits where one k_merkle wave retired (0: compiler default, 122)
+#ifndef P2V_FOLD16_HALVES
+#define P2V_FOLD16_HALVES 1
+#endif
 #ifndef P2V_FRI_WAVES
 #define P2V_FRI_WAVES 5
 #endif
@@ -769,7 +810,7 @@ extern "C" __global__ void __launch_bounds__(256) P2V_FRI_ATTR k_fri(DevCircuit 
       case 1: nv = fold_regs<1>(c, s, eoff, p, bo); break;
       case 2: nv = fold_regs<2>(c, s, eoff, p, bo); break;
       case 3: nv = fold_regs<3>(c, s, eoff, p, bo); break;
-      case 4: nv = fold_regs<4>(c, s, eoff, p, bo); break;
+      case 4: nv = P2V_FOLD16_HALVES ? fold16_halves(c, s, eoff, p, bo) : fold_regs<4>(c, s, eoff, p, bo); break;
       default: nv = fold_generic(c, s, ab, eoff, p, bo); break;
     }
     cur = nv;
