@@ -380,6 +380,41 @@ def test_literal_fri_query_values_match_oracle_trace(idx):
         assert tuple(tr[o_qfin + 2 * q:o_qfin + 2 * q + 2]) == fin, (case["name"], q, "final poly")
 
 
+def test_fold16_in_halves_is_the_same_interpolant():
+    """k_fri folds an arity-16 coset in two halves (kernels.hip fold16_halves):
+    with v the coset values in received order (vals[rev k] = v[k]), E / O the 8-point transforms
+    of v[0..7] / v[8..15] and w = omega_16, sum_k c_k b^k = (1 + b^8) E(b) + (1 - b^8) O(w^-1 b),
+    where c_k = sum_j vals_j w^(-jk).  Exact integers, against that direct sum."""
+    import random
+    rng = random.Random(16)
+    winv = finv(ROOTS[4])
+
+    def dft_horner(vals, root_inv, b):             # sum_k (sum_j vals_j root_inv^(jk)) b^k
+        n = len(vals)
+        tot, bk = (0, 0), (1, 0)
+        for k in range(n):
+            ck = (0, 0)
+            for j in range(n):
+                ck = eadd(ck, escale(pow(root_inv, j * k, P), vals[j]))
+            tot = eadd(tot, emul(bk, ck))
+            bk = emul(bk, b)
+        return tot
+
+    one = (1, 0)
+    for _ in range(12):
+        v = [(rng.randrange(P), rng.randrange(P)) for _ in range(16)]
+        b = (rng.randrange(P), rng.randrange(P))
+        vals = [None] * 16
+        for k in range(16):
+            vals[rev_bits(4, k)] = v[k]
+        direct = dft_horner(vals, winv, b)
+        half = lambda u: [u[rev_bits(3, m)] for m in range(8)]   # vals8[rev3 j] = u[j]
+        lo = dft_horner(half(v[:8]), winv * winv % P, b)
+        hi = dft_horner(half(v[8:]), winv * winv % P, escale(winv, b))
+        b8 = epow(b, 8)
+        assert eadd(emul(eadd(one, b8), lo), emul(esub(one, b8), hi)) == direct
+
+
 def test_literal_transcript_and_fri_std_n12_two_folding_steps():
     """The standard recursion shape (degree_bits 12: two arity-16 folds, a 16-coefficient final
     polynomial), freshly generated: challenges and every per-query FRI value, literal vs oracle."""
