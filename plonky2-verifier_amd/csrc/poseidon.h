@@ -57,8 +57,12 @@ __host__ __device__ __forceinline__ uint64_t mul_nc(uint64_t a, uint64_t b) {
   return gl::reduce128_nc(hi, lo);
 #endif
 }
-// x^7, latency form for the transcript chains (qposeidon.h, rposeidon.h): the branch-free
-// multiply, whose straight-line code the scheduler can interleave
+// x^7, latency forms for the transcript chains (qposeidon.h, rposeidon.h, pposeidon.h).
+// sbox_lat_br: the S-box multiply (11 VALU) with its rare -2^64 fix-up behind one wave-uniform
+// branch per stage (x^2; x^3 and x^4; x^7), as the throughput S-box (sbox_n); the row form
+// (rposeidon.h) uses it: batch-1 latency 1.734 -> 1.684 ms.  sbox_lat: the branch-free multiply
+// (14 VALU), straight-line code; the quad form keeps it (with the branch form its k_phase1 went
+// 1.93 -> 2.03 ms, profiles/r04u_sbox_lat_branch.txt).
 __host__ __device__ __forceinline__ uint64_t sbox_lat(uint64_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint64_t x2 = gl::mul_nc_dev(x, x), x3 = gl::mul_nc_dev(x, x2), x4 = gl::mul_nc_dev(x2, x2);
@@ -69,6 +73,20 @@ __host__ __device__ __forceinline__ uint64_t sbox_lat(uint64_t x) {
   gl::mul128(x, x2, hi, lo); x3 = gl::reduce128_nc(hi, lo);
   gl::mul128(x2, x2, hi, lo); x4 = gl::reduce128_nc(hi, lo);
   gl::mul128(x3, x4, hi, lo); return gl::reduce128_nc(hi, lo);
+#endif
+}
+__host__ __device__ __forceinline__ uint64_t sbox_lat_br(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t n2, n3, n4, n7;
+  uint64_t x2 = gl::mul_nc_part(x, x, n2);
+  if (__builtin_expect(n2 != 0, 0)) x2 = gl::mul_fix_neg(x2, n2);
+  uint64_t x3 = gl::mul_nc_part(x, x2, n3), x4 = gl::mul_nc_part(x2, x2, n4);
+  if (__builtin_expect((n3 | n4) != 0, 0)) { x3 = gl::mul_fix_neg(x3, n3); x4 = gl::mul_fix_neg(x4, n4); }
+  uint64_t r = gl::mul_nc_part(x3, x4, n7);
+  if (__builtin_expect(n7 != 0, 0)) r = gl::mul_fix_neg(r, n7);
+  return r;
+#else
+  return sbox_lat(x);
 #endif
 }
 // x^7

@@ -123,10 +123,10 @@ __device__ __forceinline__ uint64_t permute(uint64_t x, const Row& R, const TT& 
     uint64_t al = nkl, ah = nkh;
     lane_rc(T.rc, r + 2 <= 30 ? r + 2 : 30, R.L, nkl, nkh);   // row 30 of the split table is zero
     if (r < 4 || r >= 26) {
-      conv(R, p2::sbox_lat(x), al, ah);
+      conv(R, p2::sbox_lat_br(x), al, ah);
     } else {
       conv(R, R.L == 0 ? 0 : x, al, ah);   // words 1..11: independent of the S-box chain
-      const uint64_t s = nbcast64<0>(p2::sbox_lat(x));
+      const uint64_t s = nbcast64<0>(p2::sbox_lat_br(x));
       al += (uint64_t)(uint32_t)s * R.col0;
       ah += (s >> 32) * R.col0;
     }
