@@ -60,9 +60,9 @@ __host__ __device__ __forceinline__ uint64_t mul_nc(uint64_t a, uint64_t b) {
 // x^7, latency forms for the transcript chains (qposeidon.h, rposeidon.h, pposeidon.h).
 // sbox_lat_br: the S-box multiply (11 VALU) with its rare -2^64 fix-up behind one wave-uniform
 // branch per stage (x^2; x^3 and x^4; x^7), as the throughput S-box (sbox_n); the row form
-// (rposeidon.h) uses it: batch-1 latency 1.734 -> 1.684 ms.  sbox_lat: the branch-free multiply
+// (rposeidon.h) uses it (k_merkle_row 0.142 -> 0.134 ms).  sbox_lat: the branch-free multiply
 // (14 VALU), straight-line code; the quad form keeps it (with the branch form its k_phase1 went
-// 1.93 -> 2.03 ms, profiles/r04u_sbox_lat_branch.txt).
+// 1.93 -> 2.03 ms, profiles/r04u_sbox_lat_branch.txt, DESIGN.md §7.0).
 __host__ __device__ __forceinline__ uint64_t sbox_lat(uint64_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint64_t x2 = gl::mul_nc_dev(x, x), x3 = gl::mul_nc_dev(x, x2), x4 = gl::mul_nc_dev(x2, x2);
