@@ -491,7 +491,8 @@ def c3_leg(p2v, args, threads, dev, local, streams):
     out = c5_leg(p2v, vk, info, d_proofs, d_expect, args.batch, 1, local, dev, None, streams, True,
                  total=C3_PROOFS, chunk=C3_CHUNK, steps=C3_PASSES, warm=2,
                  note="BASELINE configs[2]: 65536 proofs of the real circuit with LookupGate/LookupTableGate (256 + 65536-entry "
-                      "tables, live lookup argument), device-resident, launches of 16384, two in flight, statuses checked on the device")
+                      "tables, live lookup argument), device-resident, launches of 16384, two in flight, statuses checked on the device; "
+                      "timed over 3 passes after 2 untimed ones ('proofs' counts all three)")
     bv = p2v.BatchVerifier(vk, local, args.batch)
     res = torch.empty(args.batch, dtype=torch.int8, device=dev)
     kt = {}
