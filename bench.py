@@ -19,7 +19,9 @@ genuine quotient: every vanishing term non-zero at zeta; with --lookups the look
 LookupGate / LookupTableGate blocks and a live lookup argument; --circuit degenerate for the
 gate-filters-0 circuit).  D distinct proofs per rank repeated into distinct
 HBM memory, 1/16 of them corrupted (initial Merkle leaf -> -1, last step sibling -> -2).
-Every timed batch's statuses are checked against the expected vector.
+Every timed batch's statuses are checked against the expected vector on the device, right after
+its launch on the launch's own stream (verified_steps), and a clock probe at both ends of each
+timed pass gives the shader clock the chip held (clock.run_clock, valu.issue.at_run_clock).
 """
 from __future__ import annotations
 
@@ -68,7 +70,7 @@ def pmc_tag():
     return max(tags) if tags else None
 
 
-def valu_roofline(kavg, ms_step, B):
+def valu_roofline(kavg, ms_step, B, run_clock_ghz=None):
     """VALU issue utilisation from the latest committed rocprofv3 VALU pass
     (profiles/<tag>_pmc_valu.json, same 4096-proof batch): issue cycles per kernel over its
     serial launch time, and for the whole (pipelined) step.  None when no PMC summary exists."""
@@ -96,7 +98,14 @@ def valu_roofline(kavg, ms_step, B):
     # dominant kernels at that clock, next to the 2.4 GHz-priced one
     eff = {k: {"clock_ghz": v["effective_clock_ghz"], "issue_frac": v["issue_frac_at_effective_clock"]}
            for k, v in pm.items() if not k.startswith("_") and v.get("effective_clock_ghz") and (v.get("duration_s") or 0) > 3e-4}
+    at_run = None
+    if run_clock_ghz:
+        # the same issue cycles against the capacity at the shader clock this run's own probes
+        # measured (s_memtime / s_memrealtime around the timed pass)
+        cap = VALU_SIMDS * run_clock_ghz
+        at_run = {"clock_ghz": run_clock_ghz, "peak": round(cap, 1), "step_frac": round(tot / (ms_step * 1e-3) / 1e9 / cap, 3)}
     return {"unit": "G SIMD issue-cycles/s", "peak": peak,
+            "at_run_clock": at_run,
             "at_effective_clock": eff or None,
             "step_achieved": round(tot / (ms_step * 1e-3) / 1e9, 1),
             "step_frac": round(tot / (ms_step * 1e-3) / 1e9 / peak, 3),
@@ -204,10 +213,21 @@ def cpu_model():
     return None
 
 
-def cpu_baseline(gc, proofs, threads, target_s=12.0, target_1_s=6.0):
-    """ORACLE (C restatement) timed on this host: the CPU path beside the GPU number, on a
-    bounded sample of about `target_s` seconds of CPU work on `threads` threads, and of about
-    `target_1_s` seconds on one thread (core count and CPU model stated)."""
+def cpu_quota_cores():
+    """The cgroup CPU quota of this process in cores (cgroup v2 cpu.max), or None if unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(gc, proofs, threads, target_s=10.0, target_1_s=6.0, target_all_s=10.0):
+    """ORACLE (C restatement) timed on this host: the CPU path beside the GPU number, on bounded
+    samples of about `target_s` seconds of CPU work on `threads` threads, `target_1_s` on one
+    thread and `target_all_s` on every core this process may run on (os.sched_getaffinity, at
+    most 256 threads) -- SURVEY.md §8(d): single-thread and all-cores, core count and CPU model
+    stated.  The top-level value is the all-cores row."""
     from support import oracle
     O = oracle()
     c = O.circuit(gc.common, gc.vkey)
@@ -226,18 +246,33 @@ def cpu_baseline(gc, proofs, threads, target_s=12.0, target_1_s=6.0):
     dt0 = run(len(ps), threads)
     k = max(len(ps), min(64 * len(ps), int(len(ps) * target_s / max(dt0, 1e-3))))
     dt = run(k, threads)
+    rate = k / dt
     # one thread: calibrated from the multi-thread rate, at least the distinct proofs once
-    k1 = max(8, min(len(ps) * 4, int(target_1_s * k / dt / max(1, threads))))
+    k1 = max(8, min(len(ps) * 4, int(target_1_s * rate / max(1, threads))))
     dt1 = run(k1, 1)
+    # all cores: one thread per core this process may use -- its affinity mask, capped by the
+    # cgroup's CPU quota where one is set (on the GPU box the mask shows 256 CPUs and the quota
+    # grants 16 cores: 256 threads there ran at 124 proofs/s against 180 on 16, gpurun_out/r05a)
+    affinity = len(os.sched_getaffinity(0))
+    quota = cpu_quota_cores()
+    n_all = max(1, min(256, affinity, int(quota + 0.5) if quota else affinity))
+    if n_all == threads:   # the multi-thread row already ran on all of them
+        k_all, dt_all = k, dt
+    else:
+        k_all = max(len(ps), min(256 * len(ps), int(target_all_s * rate / max(1, threads) * n_all)))
+        dt_all = run(k_all, n_all)
     for p in ps:
         O.L.or_proof_free(p)
     O.L.or_circuit_free(c)
-    return {"value": round(k / dt, 2), "unit": "proofs/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(),
+    return {"value": round(k_all / dt_all, 2), "unit": "proofs/s", "cores": n_all, "kind": "port",
+            "cpu_model": cpu_model(), "affinity_cpus": affinity, "cpu_quota_cores": quota,
+            "sample": f"{k_all} std-config proofs ({len(ps)} distinct, degree_bits 12) verified by oracle/oracle.c "
+                      f"on {n_all} host threads (all cores this process may use: affinity {affinity} CPUs, "
+                      f"cgroup quota {quota if quota else 'none'}) in {dt_all:.2f}s",
+            "threads_16": {"value": round(rate, 2), "cores": threads,
+                           "sample": f"{k} proofs on {threads} threads in {dt:.2f}s"},
             "single_thread": {"value": round(k1 / dt1, 2), "cores": 1,
-                              "sample": f"{k1} proofs on 1 thread in {dt1:.2f}s"},
-            "sample": f"{k} std-config proofs ({len(ps)} distinct, degree_bits 12) verified by oracle/oracle.c "
-                      f"on {threads} host threads in {dt:.2f}s"}
+                              "sample": f"{k1} proofs on 1 thread in {dt1:.2f}s"}}
 
 
 def ingest_rate(vk, proofs, threads):
@@ -301,86 +336,143 @@ def json_rate(bvs, proofs, B, steps=3):
     return out
 
 
-def bytes_rate(bvs, proofs, B, steps=3):
-    """End to end from plonky2's binary proofs (p2v_verifier_run_bytes): B proofs (the distinct
-    ones repeated) in pinned host memory, copied to the device, packed there through the circuit's
-    byte map (k_bytes_pack), then verified.  Serial, and pipelined with one host thread per verifier
-    workspace.  Reported next to the JSON and packed-word legs, never as the bench value."""
-    import threading
+def bytes_rate(bvs, proofs, B, steps=3, local=0, expect=None):
+    """End to end from plonky2's binary proofs: B proofs (the distinct ones repeated) in pinned
+    host memory, copied to the device, packed there through the circuit's byte map (k_bytes_pack),
+    then verified.  Serial: p2v_verifier_run_bytes, one batch at a time.  Pipelined:
+    p2v_verify_batch_bytes on 16 384 proofs per call (chunked copies on a copy stream, device
+    packing and verification overlapped).  Reported next to the JSON and packed-word legs, never as
+    the bench value."""
     import torch
+    import p2v
     from support import proof_bytes
     bins = [proof_bytes(p) for p in proofs]
-    texts = [bins[i % len(bins)] for i in range(B)]
-    offs = np.zeros(B + 1, dtype=np.uint64)
-    offs[1:] = np.cumsum([len(t) for t in texts])
-    blob = torch.from_numpy(np.frombuffer(b"".join(texts), dtype=np.uint8).copy()).pin_memory().numpy()
-    streams = [torch.cuda.Stream() for _ in bvs]
-    for bv, st in zip(bvs, streams):
-        res, codes = bv.run_bytes((blob, offs), stream=st.cuda_stream)
-        assert (codes == 0).all() and (res == 1).all() and bv.last_bytes_device == B
+
+    def pinned_blob(m):
+        texts = [bins[i % len(bins)] for i in range(m)]
+        offs = np.zeros(m + 1, dtype=np.uint64)
+        offs[1:] = np.cumsum([len(t) for t in texts])
+        blob = torch.from_numpy(np.frombuffer(b"".join(texts), dtype=np.uint8).copy()).pin_memory()
+        return blob, offs
+    tblob, offs = pinned_blob(B)
+    blob = tblob.numpy()
+    st = torch.cuda.Stream()
+    res, codes = bvs[0].run_bytes((blob, offs), stream=st.cuda_stream)
+    assert (codes == 0).all() and (res == 1).all() and bvs[0].last_bytes_device == B
     t = time.perf_counter()
     for _ in range(steps):
-        res, codes = bvs[0].run_bytes((blob, offs), stream=streams[0].cuda_stream)
+        res, codes = bvs[0].run_bytes((blob, offs), stream=st.cuda_stream)
     dt = (time.perf_counter() - t) / steps
     assert (res == 1).all()
     out = {"value": round(B / dt, 1), "unit": "proofs/s", "ms_per_step": round(dt * 1e3, 3),
            "note": f"{B} binary proofs ({blob.nbytes / 1e6:.0f} MB, pinned) per step: H2D + device packing (k_bytes_pack) + verify, one batch at a time"}
-    if len(bvs) > 1:
-        bad = []
-
-        def worker(bv, st):
-            for _ in range(steps):
-                r, _c = bv.run_bytes((blob, offs), stream=st.cuda_stream)
-                if not (r == 1).all():
-                    bad.append(1)
-        ths = [threading.Thread(target=worker, args=(bv, st)) for bv, st in zip(bvs, streams)]
-        t = time.perf_counter()
-        for th in ths:
-            th.start()
-        for th in ths:
-            th.join()
-        dt = time.perf_counter() - t
-        assert not bad
-        out["pipelined"] = {"value": round(B * steps * len(bvs) / dt, 1), "inflight": len(bvs),
-                            "h2d_GBps_equiv": round(blob.nbytes * steps * len(bvs) / dt / 1e9, 1)}
+    m = max(B, STREAM_PROOFS // B * B)
+    tbig, boffs = pinned_blob(m)
+    big = tbig.numpy()
+    vk = bvs[0].circuit
+    res, codes, ndev = p2v.verify_batch_bytes(vk, (big, boffs), local)   # warm: creates the pooled pipe
+    assert (codes == 0).all() and (res == 1).all() and ndev == m
+    t = time.perf_counter()
+    for _ in range(steps):
+        res, codes, ndev = p2v.verify_batch_bytes(vk, (big, boffs), local)
+        assert (codes == 0).all() and (res == 1).all() and ndev == m
+    dt = time.perf_counter() - t
+    out["pipelined"] = {"value": round(m * steps / dt, 1), "proofs_per_call": m,
+                        "h2d_GBps_equiv": round(big.nbytes * steps / dt / 1e9, 1),
+                        "note": "p2v_verify_batch_bytes: chunked H2D on a copy stream, device packing + verification overlapped, "
+                                "statuses and codes of every call checked"}
+    del tbig, tblob
     return out
 
 
-def h2d_rate(bvs, rows, B, expect, steps=3):
+STREAM_PROOFS = 16384   # proofs per call of the pipelined from-host legs (4 x the C2 batch)
+
+
+def h2d_rate(bvs, rows, B, expect, steps=3, local=0):
     """PCIe-inclusive: packed proofs in pinned host memory, H2D copy inside the timed run.
-    Serial: one batch at a time; pipelined (double-buffered): one host thread per verifier
-    workspace, each on its own stream, so one batch's copy overlaps another's verification."""
-    import threading
+    Serial: one 4096-proof batch at a time on a workspace (copy, then verify, then D2H).
+    Pipelined: p2v_verify_batch (the circuit's pooled pipeline) on 16 384 pinned proofs per call,
+    in chunks whose copies run on a copy stream of their own, overlapped with the verification
+    of the chunks before them (three in flight); every call's statuses checked."""
     import torch
+    import p2v
     host = torch.from_numpy(rows.view(np.int64)).pin_memory()
     arr = host.numpy().view(np.uint64)
-    streams = [torch.cuda.Stream() for _ in bvs]
-    for bv, st in zip(bvs, streams):
-        assert np.array_equal(bv.run(arr, stream=st.cuda_stream), expect)
+    assert np.array_equal(bvs[0].run(arr), expect)
     t = time.perf_counter()
     for _ in range(steps):
-        res = bvs[0].run(arr, stream=streams[0].cuda_stream)
+        res = bvs[0].run(arr)
     dt = (time.perf_counter() - t) / steps
     assert np.array_equal(res, expect)
     out = {"value": round(B / dt, 1), "unit": "proofs/s", "ms_per_step": round(dt * 1e3, 3),
            "note": f"{B} proofs from pinned host memory per step, H2D {rows.nbytes / 1e6:.0f} MB + verify + D2H, one batch at a time"}
-    if len(bvs) > 1:
-        bad = []
+    reps = max(1, STREAM_PROOFS // B)
+    big = torch.from_numpy(np.tile(rows, (reps, 1)).view(np.int64)).pin_memory()
+    barr = big.numpy().view(np.uint64)
+    bexp = np.tile(expect, reps)
+    vk = bvs[0].circuit
+    assert np.array_equal(p2v.verify_batch(vk, barr, local), bexp)   # warm: creates the pooled pipe
+    t = time.perf_counter()
+    for _ in range(steps):
+        res = p2v.verify_batch(vk, barr, local)
+        assert np.array_equal(res, bexp)
+    dt = time.perf_counter() - t
+    out["pipelined"] = {"value": round(barr.shape[0] * steps / dt, 1), "proofs_per_call": barr.shape[0],
+                        "h2d_GBps_equiv": round(barr.nbytes * steps / dt / 1e9, 1),
+                        "note": "p2v_verify_batch: chunked H2D on a copy stream overlapped with verification, statuses of every call checked"}
+    del big
+    return out
 
-        def worker(bv, st):
-            for _ in range(steps):
-                if not np.array_equal(bv.run(arr, stream=st.cuda_stream), expect):
-                    bad.append(1)
-        ths = [threading.Thread(target=worker, args=(bv, st)) for bv, st in zip(bvs, streams)]
+
+def dropin_leg(p2v, gc, proofs, packed, expect, local, reps=30):
+    """The reference's API is one proof per call (verifyProof, Plonk/Verifier.hs:56): the cost a
+    drop-in caller pays through the C-ABI.  cold = a fresh circuit handle's
+    first p2v_verify_batch (its pooled verifier is created then); warm = the median of later calls
+    on the same handle; workspace = the same proofs on a pre-created BatchVerifier (the batch-1
+    latency figure of DESIGN.md); verify_proof = p2v.verify_proof on the JSON text (pack + verify)."""
+    import ctypes as ct
+    out = {"unit": "ms"}
+    L = p2v.lib()
+    for n in (1, 64):
+        rows = np.ascontiguousarray(packed[:n])
+        res = np.empty(n, dtype=np.int8)
         t = time.perf_counter()
-        for th in ths:
-            th.start()
-        for th in ths:
-            th.join()
-        dt = time.perf_counter() - t
-        assert not bad
-        out["pipelined"] = {"value": round(B * steps * len(bvs) / dt, 1), "inflight": len(bvs),
-                            "h2d_GBps_equiv": round(rows.nbytes * steps * len(bvs) / dt / 1e9, 1)}
+        vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+        t_circ = time.perf_counter() - t
+        t = time.perf_counter()
+        rc = L.p2v_verify_batch(vk.handle, rows.ctypes.data, n, res.ctypes.data, local)
+        cold = time.perf_counter() - t
+        assert rc == 0 and np.array_equal(res, expect[:n])
+        warm = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            rc = L.p2v_verify_batch(vk.handle, rows.ctypes.data, n, res.ctypes.data, local)
+            warm.append(time.perf_counter() - t)
+            assert rc == 0 and np.array_equal(res, expect[:n])
+        bv = p2v.BatchVerifier(vk, local, n)
+        ws = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            r = bv.run(rows)
+            ws.append(time.perf_counter() - t)
+            assert np.array_equal(r, expect[:n])
+        del bv
+        out[f"n{n}"] = {"circuit_from_json": round(t_circ * 1e3, 3), "cold": round(cold * 1e3, 3),
+                        "warm": round(float(np.median(warm)) * 1e3, 3), "warm_min": round(min(warm) * 1e3, 3),
+                        "workspace": round(float(np.median(ws)) * 1e3, 3),
+                        "warm_over_workspace": round(float(np.median(warm)) / float(np.median(ws)), 3)}
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    text = bytes(proofs[0])
+    assert p2v.verify_proof(vk, text, device=local) is True
+    vp = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        ok = p2v.verify_proof(vk, text, device=local)
+        vp.append(time.perf_counter() - t)
+        assert ok is True
+    out["verify_proof"] = {"warm": round(float(np.median(vp)) * 1e3, 3), "json_MB": round(len(text) / 1e6, 3)}
+    out["note"] = ("C-ABI p2v_verify_batch through ctypes, host proofs in pageable memory; cold includes creating the "
+                   "circuit's pooled verifier; median of %d warm calls" % reps)
     return out
 
 
@@ -398,6 +490,30 @@ def max_over_ranks(dt, world, cpu_grp):
     t = torch.tensor([dt], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=cpu_grp)
     return float(t.item())
+
+
+def gather_over_ranks(x, world, cpu_grp):
+    """Every rank's value of one float (all_gather over the gloo side group, CPU tensors): the
+    per-rank figures behind the max-over-ranks time."""
+    if world == 1:
+        return [x]
+    import torch
+    import torch.distributed as dist
+    mine = torch.tensor([x], dtype=torch.float64)
+    parts = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(parts, mine, group=cpu_grp)
+    return [float(p.item()) for p in parts]
+
+
+def per_rank_summary(proofs, own_s, world, cpu_grp, clock_ghz=None):
+    """Per-rank throughput (each rank's own proofs over its own time, before the closing barrier),
+    min / max and the imbalance 1 - min/max; with clock_ghz, every rank's shader clock over its pass."""
+    rates = [proofs / t if t > 0 else 0.0 for t in gather_over_ranks(own_s, world, cpu_grp)]
+    out = {"proofs_per_s": [round(r, 1) for r in rates], "min": round(min(rates), 1), "max": round(max(rates), 1),
+           "imbalance": round(1.0 - min(rates) / max(rates), 4) if max(rates) > 0 else None}
+    if clock_ghz is not None:
+        out["clock_ghz"] = [round(c, 4) for c in gather_over_ranks(float(clock_ghz), world, cpu_grp)]
+    return out
 
 
 def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, cpu_grp, streams, tiled, steps=1, stagger=0,
@@ -450,16 +566,19 @@ def c5_leg(p2v, vk, info, d_proofs, d_expect, B, world, local, dev, cpu_grp, str
     for _ in range(steps):
         one_pass(True)
     torch.cuda.synchronize(dev)
+    own = time.perf_counter() - t   # this rank's own time (before the closing barrier)
     if world > 1:
         dist.barrier(group=cpu_grp)
     dt = time.perf_counter() - t
     ok = bool(okf[0].item()) and bool(okf[1].item())
     dt = max_over_ranks(dt, world, cpu_grp)
+    per_rank = per_rank_summary(n * steps, own, world, cpu_grp)
+    ok_all = all(v > 0 for v in gather_over_ranks(1.0 if ok else 0.0, world, cpu_grp))
     del big, bvs, res
     torch.cuda.empty_cache()
     return {"proofs": total * steps, "value": round(total * steps / dt, 1), "unit": "proofs/s",
             "per_gpu": round(total * steps / dt / world, 1), "seconds": round(dt, 4), "n_gpus": world,
-            "shard_per_gpu": n, "launch_proofs": rows, "verified_all": ok,
+            "per_rank": per_rank, "shard_per_gpu": n, "launch_proofs": rows, "verified_all": ok_all,
             "note": note or ("BASELINE configs[4]: 1M std proofs sharded over the ranks (no data-path collective), "
                              "launches of <= 131072 device-resident proofs, two in flight per GPU, every launch's statuses checked on "
                              "the device; time = max over ranks")}
@@ -534,7 +653,8 @@ def main():
     ap.add_argument("--lookups", type=int, default=0,
                     help="0: standard recursion circuit (C2); 2: + LookupGate/LookupTableGate with a 256-entry and a 2^16-entry table (C3 circuit)")
     ap.add_argument("--transcript", choices=("auto", "row", "quad", "pair", "lane"), default="auto",
-                    help="transcript layout (P2V_TRANSCRIPT): auto = row below 2048 proofs, quad from 2048 on")
+                    help="transcript layout (P2V_TRANSCRIPT): auto = row below 2048 proofs per launch, quad from 2048, "
+                         "lane from 16384 (P2V_LANE_MIN)")
     ap.add_argument("--single-stream", action="store_true", help="P2V_SINGLE_STREAM=1: each workspace on one stream (no side stream)")
     ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES for this process (0: the runtime's default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -623,16 +743,23 @@ def main():
             bvs[j].chain(bvs[j - 1])
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nv - 1)]
 
+    NPROBE = 256   # one-wave clock-probe workgroups (spread over every XCD)
+
     def timed(k, pipelined):
         """k steps; pipelined: batch i goes to workspace/stream i % nv without host sync, so
         up to nv batches are in flight (batch i+1's transcript overlaps batch i's Merkle
-        work); serial: one workspace, synchronous, per-kernel times recorded."""
+        work); serial: one workspace, synchronous, per-kernel times recorded.  Every step's
+        statuses are compared with the expected vector on the device, on the launch's own stream,
+        right after it (p2v_count_mismatches: a per-stream mismatch counter and check count), and
+        a clock probe at each end of the pass gives the shader clock the chip held over it."""
         ktimes = {}
         # device-side clock of the same pass (VERDICT r3 item 1): one timing event per stream
         # before its first launch and one after every launch, on the launch's own stream
         nst = nv if pipelined else 1
         ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(nst)]
         ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(k)]
+        cnt = torch.zeros((nst, 2), dtype=torch.int64, device=dev)   # per stream: mismatches, checks run
+        stamps = torch.zeros((2, NPROBE, 3), dtype=torch.int64, device=dev)
         host_enq = []
         if world > 1:
             dist.barrier(group=cpu_grp)
@@ -640,16 +767,22 @@ def main():
         t = time.perf_counter()
         for j in range(nst):
             ev0[j].record(streams[j])
+        p2v.clock_probe(stamps[0].data_ptr(), NPROBE, streams[0].cuda_stream)
         for i in range(k):
             j = i % nv if pipelined else 0
             bvs[j].run_device(d_proofs.data_ptr(), B, d_res[j].data_ptr(), stream=streams[j].cuda_stream, sync=not pipelined,
                               tiled=lay_tiled, lookahead=bool(args.lookahead))
+            p2v.count_mismatches(d_res[j].data_ptr(), d_expect.data_ptr(), B, cnt[j].data_ptr(), streams[j].cuda_stream)
             ev1[i].record(streams[j])
             host_enq.append(time.perf_counter() - t)
             if not pipelined:
                 for name, v in bvs[0].last_timings().items():
                     ktimes.setdefault(name, []).append(v)
+        for j in range(1, nst):
+            streams[0].wait_stream(streams[j])
+        p2v.clock_probe(stamps[1].data_ptr(), NPROBE, streams[0].cuda_stream)
         torch.cuda.synchronize(dev)
+        own = time.perf_counter() - t   # this rank's own time, before the closing barrier
         if world > 1:
             dist.barrier(group=cpu_grp)
         dt = time.perf_counter() - t
@@ -658,6 +791,10 @@ def main():
         starts = [ev0[0].elapsed_time(e) for e in ev0]
         dev_ms = max(done) - min(starts)
         gaps = np.diff(np.array([min(starts)] + done))
+        st = stamps.cpu().numpy().view(np.uint64)
+        run_clock = p2v.clock_from_probes(st[0], st[1])
+        c = cnt.cpu().numpy()
+        check = {"steps": int(c[:, 1].sum()), "mismatches": int(c[:, 0].sum())}
         clock = {"host_ms": round(dt * 1e3, 3), "device_ms": round(dev_ms, 3),
                  "device_over_host": round(dev_ms / (dt * 1e3), 4),
                  "step_ms": {"mean": round(float(gaps.mean()), 4), "min": round(float(gaps.min()), 4),
@@ -665,8 +802,9 @@ def main():
                              "first": [round(float(x), 4) for x in gaps[:4]], "last": [round(float(x), 4) for x in gaps[-4:]]},
                  "host_enqueue_ms": {"mean": round(float(np.mean(np.diff([0.0] + host_enq))) * 1e3, 4),
                                      "max": round(float(np.max(np.diff([0.0] + host_enq))) * 1e3, 4),
-                                     "last_enqueued_at": round(host_enq[-1] * 1e3, 3)}}
-        return max_over_ranks(dt, world, cpu_grp), ktimes, clock
+                                     "last_enqueued_at": round(host_enq[-1] * 1e3, 3)},
+                 "run_clock": run_clock}
+        return max_over_ranks(dt, world, cpu_grp), ktimes, clock, own, check
 
     # Order: the W warm-up steps run immediately before the headline
     # (pipelined) pass, with no host work between them, because the GPU's clock drops within
@@ -680,17 +818,24 @@ def main():
         bvs[i % nv].run_device(d_proofs.data_ptr(), B, d_res[i % nv].data_ptr(), stream=streams[i % nv].cuda_stream, sync=False,
                                tiled=lay_tiled, lookahead=bool(args.lookahead))
     if nv > 1:
-        dt, _, clock = timed(args.steps, True)
+        dt, _, clock, own, check = timed(args.steps, True)
         ok = all(bool((r == d_expect).all()) for r in d_res[:min(nv, args.steps)])
         for r in d_res:
             r.zero_()
     # serial pass: per-kernel durations (HIP events recorded on the run's streams inside libp2v)
-    dt_serial, ktimes, clock_serial = timed(args.steps, False)
+    dt_serial, ktimes, clock_serial, own_serial, check_serial = timed(args.steps, False)
     if nv > 1:
         ok = ok and bool((d_res[0] == d_expect).all())
     else:
-        dt, clock = dt_serial, clock_serial
+        dt, clock, own, check = dt_serial, clock_serial, own_serial, check_serial
         ok = bool((d_res[0] == d_expect).all())
+    # every timed step of both passes checked on the device, on every rank
+    ok = ok and check["mismatches"] == 0 and check["steps"] == args.steps
+    ok = ok and check_serial["mismatches"] == 0 and check_serial["steps"] == args.steps
+    ok = all(v > 0 for v in gather_over_ranks(1.0 if ok else 0.0, world, cpu_grp))
+    verified_steps = int(min(gather_over_ranks(float(check["steps"] if check["mismatches"] == 0 else 0), world, cpu_grp)))
+    run_clock = (clock.get("run_clock") or {}).get("clock_ghz")
+    per_rank = per_rank_summary(B * args.steps, own, world, cpu_grp, run_clock)
     total = B * args.steps * world
     value = total / dt
     kavg = {k: float(np.mean(v)) for k, v in ktimes.items()}
@@ -753,10 +898,15 @@ def main():
                          "note": "binding resource: integer VALU issue (Poseidon), valu_issue_frac = valu.issue.step_frac; "
                                  "achieved/peak/frac: the dominant kernel's algorithmic HBM bytes over its launch time"},
             "valu": {"perms_per_proof": ppp, "perm_rate_G": round(value / world * ppp / 1e9, 3),
-                     "issue": valu_roofline(kavg, dt / args.steps * 1e3, B)
+                     "issue": valu_roofline(kavg, dt / args.steps * 1e3, B, run_clock)
                      if (real and info.degree_bits == 12 and not args.lookups and not args.ext and not arities) else None},   # the PMC pass's own workload only
             "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
             "verified_all": ok,
+            "verified_steps": verified_steps,
+            "verification": {"pipelined": check, "serial": check_serial,
+                             "note": "every timed step's statuses compared with the expected vector on the device, on the "
+                                     "launch's stream right after it (p2v_count_mismatches); steps = checks that ran, min over ranks"},
+            "per_rank": per_rank,
         }
         if out["valu"]["issue"]:
             out["roofline"]["valu_issue_frac"] = out["valu"]["issue"]["step_frac"]
@@ -765,10 +915,11 @@ def main():
         if c3 is not None:
             out["c3"] = c3
         if world == 1 and not args.quick:
+            out["dropin"] = dropin_leg(p2v, gc, proofs, rows, expect, local)
             out["ingest"] = ingest_rate(vk, proofs, threads)
-            out["h2d_end_to_end"] = h2d_rate(bvs, rows, B, expect)
+            out["h2d_end_to_end"] = h2d_rate(bvs, rows, B, expect, local=local)
             out["json_end_to_end"] = json_rate(bvs, proofs, B)
-            out["bytes_end_to_end"] = bytes_rate(bvs, proofs, B)
+            out["bytes_end_to_end"] = bytes_rate(bvs, proofs, B, local=local)
         if world == 1 and not args.no_cpu_baseline and not args.quick:
             out["cpu_baseline"] = cpu_baseline(gc, proofs, threads)
         print(json.dumps(out), flush=True)

@@ -33,6 +33,7 @@ import Control.Exception (finally)
 import Control.Monad (when, forM, forM_)
 import Data.Bits ((.&.))
 import Data.Char (ord)
+import Data.IORef (IORef, newIORef, readIORef, atomicModifyIORef')
 import Data.Int (Int8, Int32, Int64)
 import Data.Word (Word8, Word32, Word64)
 import Foreign
@@ -214,6 +215,30 @@ loadGpuCircuit vkey = withArrayLen (circuitWords vkey) $ \n ws ->
     when (rc /= 0) $ throwLast "p2v_circuit_from_words"
     GpuCircuit <$> (peek out >>= newForeignPtr c_circuit_free)
 
+-- | The circuits loaded by 'verifyProof' / 'verifyProofBatch' and the intermediates, keyed by
+-- their word encoding, most recent first (at most 'circuitCacheSize').  A repeated call with the
+-- same 'VerifierCircuitData' reuses the libp2v circuit handle, and with it the verifier libp2v
+-- keeps per circuit and device (p2v_verify_batch's pool, include/p2v.h): no re-decode and no
+-- device allocation per call (VERDICT r4 item 2).  A handle dropped from the cache is freed by
+-- its finalizer once no call still uses it.
+circuitCache :: IORef [([Word64], GpuCircuit)]
+circuitCache = unsafePerformIO (newIORef [])
+{-# NOINLINE circuitCache #-}
+
+circuitCacheSize :: Int
+circuitCacheSize = 4
+
+cachedGpuCircuit :: VerifierCircuitData -> IO GpuCircuit
+cachedGpuCircuit vkey = do
+  let ws = circuitWords vkey
+  hit <- lookup ws <$> readIORef circuitCache
+  case hit of
+    Just c  -> pure c
+    Nothing -> do
+      c <- loadGpuCircuit vkey
+      atomicModifyIORef' circuitCache (\cs -> (take circuitCacheSize ((ws, c) : filter ((/= ws) . fst) cs), ()))
+      pure c
+
 -- | The same with opt-in plonky2 conventions the reference does not implement (P2V_EXT_* of
 -- include/p2v.h: 1 fri_params arities / MinSize, 2 hiding salts, 4 hash_or_noop leaves).
 loadGpuCircuitExt :: Word32 -> VerifierCircuitData -> IO GpuCircuit
@@ -307,7 +332,7 @@ withShapeVariant c ws m k = alloca $ \np -> alloca $ \nf -> alloca $ \out -> do
 -- (the reference's proofChallenges reads both lists at any length).
 traceOf :: VerifierCircuitData -> ProofWithPublicInputs -> IO ((Int, Int, Int, Bool), [Word64])
 traceOf vkey proof = do
-  GpuCircuit fc <- loadGpuCircuit vkey
+  GpuCircuit fc <- cachedGpuCircuit vkey
   withForeignPtr fc $ \c -> withArrayLen (proofWords proof) $ \m ws -> do
     t <- traceWith c ws m
     case t of
@@ -393,11 +418,12 @@ verifyProofBatch vkey = verifyProofBatchOn [0] vkey
 -- | The same, sharded over several GPUs of the node.
 verifyProofBatchOn :: [Int] -> VerifierCircuitData -> [ProofWithPublicInputs] -> IO [Bool]
 verifyProofBatchOn devices vkey proofs = do
-  c <- loadGpuCircuit vkey
+  c <- cachedGpuCircuit vkey
   verifyWithCircuit c devices proofs
 
 -- | Same type and meaning as 'Plonk.Verifier.verifyProof' (src/Plonk/Verifier.hs:56): True,
--- False, or the @error@ the reference raises.
+-- False, or the @error@ the reference raises.  A repeated call on the same circuit costs the
+-- kernels (libp2v's pooled verifier, the cached circuit handle), not a workspace.
 verifyProof :: VerifierCircuitData -> ProofWithPublicInputs -> Bool
 verifyProof vkey proof = unsafePerformIO $ head <$> verifyProofBatch vkey [proof]
 {-# NOINLINE verifyProof #-}

@@ -281,16 +281,32 @@ int  p2v_verifier_run_bytes(p2v_verifier* v, const uint8_t* blob, const uint64_t
 int  p2v_verifier_pack_bytes(p2v_verifier* v, const uint8_t* blob, const uint64_t* offsets, size_t n,
                              int32_t* codes, size_t* n_device, uint64_t* words, void* stream);
 
-/* One-shot convenience: create a verifier on `device`, verify, free. */
+/* One-shot form of verifyProof over a batch in host memory (proof-major packed rows), on `device`.
+ * The circuit handle keeps the verifier it runs on (a pool per circuit and device, created on
+ * first use, freed with the circuit), so a repeated call -- a drop-in verifyProof per proof --
+ * costs the kernels and the copies, not a workspace.  Up to 64 proofs run as one latency-mode
+ * launch; larger batches are verified in chunks (about n/8, 256..16384 proofs) whose H2D copies
+ * run on a copy stream of their own, overlapped with the verification of the chunks before them
+ * (three chunk buffers in flight).  Thread-safe: concurrent calls on one circuit use distinct
+ * pooled verifiers.  Replaces: map (verifyProof vkey) (Plonk/Verifier.hs:56-65). */
 int  p2v_verify_batch(const p2v_circuit* c, const uint64_t* proofs, size_t n,
                       int8_t* results, int device);
 
+/* The same for plonky2 binary proofs (the p2v_pack_proof_bytes format): blob + offsets[n + 1] in
+ * host memory (pinned for the full link rate).  Per chunk the bytes are copied on the copy stream,
+ * packed on the device and verified, chunks overlapped as above; proofs the device packer does not
+ * take are packed by the host reader and verified afterwards, so results / codes / n_device are
+ * those of p2v_verifier_run_bytes.  chunk: proofs per chunk (0: automatic). */
+int  p2v_verify_batch_bytes(const p2v_circuit* c, const uint8_t* blob, const uint64_t* offsets, size_t n,
+                            int8_t* results, int32_t* codes, size_t* n_device, int device, size_t chunk);
+
 /* Single-process multi-GPU form of p2v_verify_batch: the batch (host memory,
  * proof-major) is split into ndevices contiguous near-equal shards, shard i verified on
- * devices[i] (a device may repeat), in chunks of at most `chunk` proofs (0: 16384) copied H2D
- * per chunk.  Each shard has two workers (a host thread, stream and verifier each) taking
- * alternate chunks, so one chunk's copy overlaps another's verification.  Proofs are independent, so there is
- * no cross-device traffic.  On failure returns the first failing shard's code and message.
+ * devices[i] (a device may repeat) by the circuit's pooled pipeline for that device, in chunks of
+ * `chunk` proofs (0: automatic, as p2v_verify_batch) whose H2D copies overlap the verification of
+ * the chunks before them.  One host thread per shard (none for a single shard).  Proofs are
+ * independent, so there is no cross-device traffic.  On failure returns the first failing
+ * shard's code and message.
  * Replaces: map (verifyProof vkey) over a batch (Plonk/Verifier.hs:56-65) on N GPUs. */
 int  p2v_verify_batch_devices(const p2v_circuit* c, const uint64_t* proofs, size_t n, int8_t* results,
                               const int* devices, int ndevices, size_t chunk);
@@ -305,9 +321,25 @@ int  p2v_verify_batch_devices(const p2v_circuit* c, const uint64_t* proofs, size
  *   op 4: out[12i..] = M a[12i..] + (b[0..12) + 2^32 b[12..24)) mod p, not canonicalised: one MDS
  *         layer with the next round's constants as the permutation computes it (the row
  *         reduction's rare carry fix-up included; b, 24 words, shared by all items) (Poseidon.hs:100-101)
+ *   ops 5-8: out[i] = a[i]^7 mod p, canonical, through each S-box form with its rare -2^64
+ *         fix-up (Poseidon.hs:92-96): 5 the throughput permutation's (one S-box), 6 its grouped
+ *         pair (a[i], b[i]) -> out[2i], out[2i+1], 7 the row form's, 8 the quad / pair forms'
+ *   ops 9-11: out[12i..] = the Poseidon permutation of a[12i..] in the latency forms of the
+ *         transcript and the small-batch Merkle paths: 9 row (16 lanes per state), 10 quad
+ *         (4 lanes), 11 pair (2 lanes)                     (Hash/Poseidon.hs:42-46)
  * Inputs may be any u64 (values >= p are congruent, as the reference reads them).
  * Test hook for the parity suite (edge values the synthetic proofs never produce). */
 int  p2v_selftest(int device, int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n);
+
+/* Measurement helpers (bench.py; device pointers, enqueued on `stream`, no host sync):
+ * p2v_count_mismatches: counters[0] += #{i < n : results[i] != expect[i]}, counters[1] += 1 --
+ *   a device-side status check after each timed launch, so every timed batch is verified
+ *   without a host round trip (counters: 2 u64 in device memory, zeroed by the caller).
+ * p2v_clock_probe: nblocks one-wave workgroups; workgroup b writes (XCC id, s_memtime,
+ *   s_memrealtime) to stamps[3b .. 3b+2].  Two probes around a timed pass give the shader clock
+ *   the chip held over it per XCD: d(memtime) / d(memrealtime) x 100 MHz. */
+int  p2v_count_mismatches(const int8_t* results, const int8_t* expect, size_t n, uint64_t* counters, void* stream);
+int  p2v_clock_probe(uint64_t* stamps, int nblocks, void* stream);
 
 /* Per-launch timing of the last run (milliseconds, from HIP events on the run's stream):
  * out[k] for kernel k in the order named by p2v_kernel_names(). Returns count. */

@@ -44,6 +44,9 @@ extern "C" __global__ void k_lut(DevCircuit);
 extern "C" __global__ void k_vanish_final(DevCircuit);
 extern "C" __global__ void k_status(DevCircuit, int8_t*, uint64_t*, int64_t);
 extern "C" __global__ void k_selftest(int, const uint64_t*, const uint64_t*, uint64_t*, int64_t);
+extern "C" __global__ void k_selftest_forms(int, const uint64_t*, uint64_t*, int64_t);
+extern "C" __global__ void k_count_mismatches(const int8_t*, const int8_t*, int64_t, unsigned long long*);
+extern "C" __global__ void k_clock_probe(unsigned long long*);
 extern "C" __global__ void k_json_pack(const uint8_t*, const uint64_t*, int, const uint8_t*, int64_t, const int32_t*, int64_t, uint64_t*, int64_t, int8_t*);
 extern "C" __global__ void k_bytes_pack(const uint8_t*, const uint64_t*, int, const int64_t*, const int64_t*, const int64_t*, int,
                                         const int64_t*, const uint8_t*, int, int64_t, int64_t, int64_t, uint64_t*, int64_t, int8_t*);
@@ -67,7 +70,16 @@ struct DevBuf {
 };
 }  // namespace
 
-struct p2v_circuit { Circuit c; };
+struct HostPipe;
+// The circuit handle also owns the verifiers the one-shot entry points (p2v_verify_batch,
+// p2v_verify_batch_devices) run on, kept across calls (a drop-in verifyProof
+// call must not re-create workspaces, streams and events).  Read-only for the circuit itself.
+struct p2v_circuit {
+  Circuit c;
+  mutable std::mutex pool_mu;
+  mutable std::vector<HostPipe*> pool;   // idle and busy pipes of every device
+  ~p2v_circuit();
+};
 
 namespace {
 template <class T>
@@ -166,6 +178,60 @@ struct p2v_verifier {
   // to pageable memory would stage through the runtime and stall the other streams' work
   int8_t* h_res = nullptr;
 };
+
+// One device's pipeline for batches in host memory (p2v_verify_batch / _devices): a verifier, a
+// compute stream and a copy stream, and a ring of kRing device chunk buffers, so chunk i+1's H2D
+// copy (copy stream) overlaps chunk i's verification (compute stream) and up to kRing chunks are in
+// flight.  Owned by the circuit's pool, reused across calls.
+struct HostPipe {
+  static constexpr int kRing = 3;
+  int device = -1;
+  size_t cap = 0;                 // the verifier's max_batch = the largest chunk
+  p2v_verifier* v = nullptr;
+  hipStream_t st = nullptr, cs = nullptr;
+  DevBuf ring[kRing];
+  hipEvent_t copied[kRing] = {}, freed[kRing] = {};
+  bool have_ring = false;
+  DevBuf dres;                    // device statuses of the whole call (grown on demand)
+  int8_t* h_res = nullptr;        // pinned staging for them
+  size_t h_res_cap = 0;
+  // binary-proof ingest (p2v_verify_batch_bytes): per ring slot the chunk's bytes and offsets on
+  // the device, the offsets' host copy (rewritten once the slot's previous copy is done), and the
+  // device packer's ok flags of the whole call
+  DevBuf bbytes[kRing], boffs[kRing], dok;
+  std::vector<uint64_t> hoffs[kRing];
+  int8_t* h_ok = nullptr;
+  size_t h_ok_cap = 0;
+  bool busy = false;
+};
+
+namespace {
+void pipe_free(HostPipe* p) {
+  if (!p) return;
+  (void)hipSetDevice(p->device);
+  if (p->st) (void)hipStreamSynchronize(p->st);
+  if (p->cs) (void)hipStreamSynchronize(p->cs);
+  for (int k = 0; k < HostPipe::kRing; k++) {
+    p->ring[k].free_();
+    if (p->copied[k]) (void)hipEventDestroy(p->copied[k]);
+    if (p->freed[k]) (void)hipEventDestroy(p->freed[k]);
+  }
+  p->dres.free_();
+  p->dok.free_();
+  for (int k = 0; k < HostPipe::kRing; k++) { p->bbytes[k].free_(); p->boffs[k].free_(); }
+  if (p->h_res) (void)hipHostFree(p->h_res);
+  if (p->h_ok) (void)hipHostFree(p->h_ok);
+  if (p->st) (void)hipStreamDestroy(p->st);
+  if (p->cs) (void)hipStreamDestroy(p->cs);
+  p2v_verifier_free(p->v);
+  delete p;
+}
+constexpr int kPoolIdleMax = 4;   // idle pipes kept per (circuit, device)
+}  // namespace
+
+p2v_circuit::~p2v_circuit() {
+  for (HostPipe* p : pool) pipe_free(p);
+}
 
 extern "C" {
 
@@ -279,7 +345,8 @@ int p2v_circuit_shape_variant(const p2v_circuit* pc, int num_public_inputs, int 
   if (!pc || !out) return fail(P2V_E_ARG, "null argument");
   *out = nullptr;
   try {
-    auto* v = new p2v_circuit{circuit_shape_variant(pc->c, num_public_inputs, final_poly_len)};
+    auto* v = new p2v_circuit();
+    v->c = circuit_shape_variant(pc->c, num_public_inputs, final_poly_len);
     *out = v;
     return P2V_OK;
   } catch (const CircuitError& e) { return fail(P2V_E_SHAPE, e.what()); }
@@ -655,16 +722,20 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   // phase 1: transcript waves + leaf-hash waves in one launch (the leaf sponges do not
   // depend on the challenges, so they fill the GPU while the serial transcripts run)
   // transcript form: the row form (16 lanes/proof) has the lowest latency, the quad form
-  // (4 lanes/proof) the lowest total cost; large batches hide the quad latency behind
-  // their leaf hashing.  P2V_TRANSCRIPT=row|quad overrides (measurement).
-  // from lane_min_batch on, the lane form (one lane per proof, ~half of the quad's issue cycles per
-  // proof, a ~5.7 ms chain): the batch's leaf hashing in the same launch outlasts the chain, so it
-  // costs no latency (DESIGN.md §7.0: C5's 131 072-proof launches +2.9 %, C3's 16 384 +1 %)
+  // (4 lanes/proof) a lower total cost; batches from 2048 proofs hide the quad latency behind
+  // their leaf hashing.  P2V_TRANSCRIPT=row|quad|lane|pair overrides (measurement).
+  // From lane_min_batch on, the lane form (one lane per proof, about half of the quad's issue
+  // cycles per proof: 85.9 M against 169.4 M VALU instructions per 4096 proofs, DESIGN.md §7.0,
+  // with a ~5.7 ms chain): the batch's leaf hashing in the same launch outlasts the chain, so it
+  // costs no latency (C5's 131 072-proof launches +2.9 %, C3's 16 384 +1 %)
   int tl = d.B >= v->lane_min_batch ? 1 : d.B >= v->quad_min_batch ? 4 : 16;
   if (v->transcript_mode == 1) tl = 16;
   else if (v->transcript_mode == 2) tl = 4;
   else if (v->transcript_mode == 3) tl = 1;
   else if (v->transcript_mode == 4) tl = 2;
+  // P2V_PHASE1=excl (measurement) takes the row or quad transcript only: the lane / pair forms
+  // fall back to the quad form here, before anything is enqueued
+  if (v->split_phase1 == 2 && tl <= 2) tl = 4;
   const int nt_blocks = (tl * d.B + 255) / 256;
   const int leaf_units = d.Q * d.T * NPB;
   // staggered workspaces (p2v_verifier_chain): phase 1 after the linked workspace's latest one
@@ -713,7 +784,6 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     // the transcripts first, on st, so their waves claim empty SIMDs before the leaf waves land
     HCK(hipEventRecord(v->dep_p1, st));   // the batch is ready on st
     T0(9, st);
-    if (tl <= 2) return fail(P2V_E_ARG, "P2V_PHASE1=excl takes the row or quad transcript only");
     k_transcript_x<<<nt_blocks, 256, 0, st>>>(d, tl);
     DBG("k_transcript_x", st);
     T1(9, st);
@@ -861,6 +931,97 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   return P2V_OK;
 }
 
+// a pipe of circuit c on `device` whose verifier holds `cap` proofs: an idle one of the pool (the
+// smallest that fits), else a new one
+static int pipe_acquire(const p2v_circuit* c, int device, size_t cap, HostPipe** out) {
+  *out = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(c->pool_mu);
+    HostPipe* best = nullptr;
+    for (HostPipe* p : c->pool)
+      if (!p->busy && p->device == device && p->cap >= cap && (!best || p->cap < best->cap)) best = p;
+    if (best) { best->busy = true; *out = best; return P2V_OK; }
+  }
+  auto* p = new HostPipe();
+  p->device = device; p->cap = cap;
+  int rc = P2V_OK;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&p->st, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&p->cs, hipStreamNonBlocking) != hipSuccess)
+    rc = fail(P2V_E_DEVICE, "stream creation on device " + std::to_string(device));
+  if (rc == P2V_OK) rc = p2v_verifier_create(c, device, cap, &p->v);
+  if (rc != P2V_OK) { pipe_free(p); return rc; }
+  p->busy = true;
+  std::lock_guard<std::mutex> lk(c->pool_mu);
+  c->pool.push_back(p);
+  *out = p;
+  return P2V_OK;
+}
+
+static void pipe_release(const p2v_circuit* c, HostPipe* p, bool broken) {
+  HostPipe* drop = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(c->pool_mu);
+    p->busy = false;
+    int idle = 0;
+    for (HostPipe* q : c->pool) idle += (!q->busy && q->device == p->device) ? 1 : 0;
+    if (broken || idle > kPoolIdleMax) {   // a pipe whose run failed is not reused
+      c->pool.erase(std::remove(c->pool.begin(), c->pool.end(), p), c->pool.end());
+      drop = p;
+    }
+  }
+  pipe_free(drop);
+}
+
+// verify m proofs (proof-major rows in host memory) on pipe p: one run for a single chunk (the
+// latency path: H2D, kernels, D2H on the pipe's stream); otherwise chunks of <= p->cap proofs
+// through the ring, copies on the copy stream, verification on the compute stream, statuses
+// accumulated on the device and copied back once.
+static int pipe_run(HostPipe* p, const uint64_t* src, size_t m, int8_t* results, size_t W, size_t chunk) {
+  HCK(hipSetDevice(p->device));
+  if (m <= chunk) return p2v_verifier_run(p->v, src, m, results, nullptr, p->st, 0);
+  if (!p->have_ring) {
+    for (int k = 0; k < HostPipe::kRing; k++) {
+      HCK(p->ring[k].alloc(p->cap * W * 8));
+      HCK(hipEventCreateWithFlags(&p->copied[k], hipEventDisableTiming));
+      HCK(hipEventCreateWithFlags(&p->freed[k], hipEventDisableTiming));
+    }
+    p->have_ring = true;
+  }
+  if (p->dres.bytes < m) { p->dres.free_(); HCK(p->dres.alloc(m)); }
+  if (p->h_res_cap < m) {
+    if (p->h_res) (void)hipHostFree(p->h_res);
+    p->h_res = nullptr; p->h_res_cap = 0;
+    HCK(hipHostMalloc((void**)&p->h_res, m));
+    p->h_res_cap = m;
+  }
+  const size_t nch = (m + chunk - 1) / chunk;
+  for (size_t i = 0; i < nch; i++) {
+    const int b = (int)(i % HostPipe::kRing);
+    const size_t off = i * chunk, len = std::min(chunk, m - off);
+    if (i >= (size_t)HostPipe::kRing) HCK(hipStreamWaitEvent(p->cs, p->freed[b], 0));   // its last reader is done
+    HCK(hipMemcpyAsync(p->ring[b].p, src + off * W, len * W * 8, hipMemcpyHostToDevice, p->cs));
+    HCK(hipEventRecord(p->copied[b], p->cs));
+    HCK(hipStreamWaitEvent(p->st, p->copied[b], 0));
+    const int rc = p2v_verifier_run(p->v, (const uint64_t*)p->ring[b].p, len, (int8_t*)p->dres.p + off, nullptr, p->st,
+                                    P2V_FLAG_INPUT_DEVICE | P2V_FLAG_RESULT_DEVICE | P2V_FLAG_NO_SYNC);
+    if (rc != P2V_OK) return rc;
+    HCK(hipEventRecord(p->freed[b], p->st));
+  }
+  HCK(hipMemcpyAsync(p->h_res, p->dres.p, m, hipMemcpyDeviceToHost, p->st));
+  HCK(hipStreamSynchronize(p->st));
+  memcpy(results, p->h_res, m);
+  return P2V_OK;
+}
+
+// the chunk size of a shard of m proofs: the given one, or (0) about an eighth of the shard in
+// multiples of 256 between 256 and 16384, so a batch of a few thousand proofs still has several
+// chunks in flight and a large one keeps its launches large
+static size_t auto_chunk(size_t m, size_t chunk) {
+  if (chunk) return chunk;
+  const size_t c = (m / 8 + 255) / 256 * 256;
+  return std::min<size_t>(16384, std::max<size_t>(256, c));
+}
+
 int p2v_verify_batch_devices(const p2v_circuit* c, const uint64_t* proofs, size_t n, int8_t* results,
                              const int* devices, int ndevices, size_t chunk) {
   if (!c || !devices || ndevices <= 0 || (n && (!proofs || !results))) return fail(P2V_E_ARG, "null argument / no devices");
@@ -869,38 +1030,37 @@ int p2v_verify_batch_devices(const p2v_circuit* c, const uint64_t* proofs, size_
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(P2V_E_NODEVICE, "no HIP device available: libp2v verifies on MI355X only (no CPU fallback)");
   for (int i = 0; i < ndevices; i++)
     if (devices[i] < 0 || devices[i] >= ndev) return fail(P2V_E_ARG, "bad device index " + std::to_string(devices[i]));
-  if (chunk == 0) chunk = 16384;
   const size_t W = (size_t)c->c.L.words;
   const int shards = (int)std::min<size_t>((size_t)ndevices, n);
-  // two workers per shard (own host thread, stream and verifier), taking alternate chunks, so
-  // one chunk's H2D copy overlaps the other's verification on the same device
-  constexpr int kWorkers = 2;
-  std::vector<int> rcs(shards * kWorkers, P2V_OK);
-  std::vector<std::string> msgs(shards * kWorkers);
-  auto work = [&](int s, int k) {
+  std::vector<int> rcs(shards, P2V_OK);
+  std::vector<std::string> msgs(shards);
+  auto work = [&](int s) {
     const size_t base = n / shards, extra = n % shards;   // p2v.shard_bounds
     const size_t a = s * base + std::min<size_t>(s, extra), b = a + base + ((size_t)s < extra ? 1 : 0);
-    if (a + k * chunk >= b) return;   // no chunk for this worker
-    int rc = P2V_OK;
-    p2v_verifier* v = nullptr;
-    hipStream_t st = nullptr;
-    if (hipSetDevice(devices[s]) != hipSuccess || hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
-      rc = fail(P2V_E_DEVICE, "stream creation on device " + std::to_string(devices[s]));
-    if (rc == P2V_OK) rc = p2v_verifier_create(c, devices[s], std::min(chunk, b - a), &v);
-    for (size_t i = a + k * chunk; rc == P2V_OK && i < b; i += kWorkers * chunk)
-      rc = p2v_verifier_run(v, proofs + i * W, std::min(chunk, b - i), results + i, nullptr, st, 0);
-    if (rc != P2V_OK) msgs[s * kWorkers + k] = g_err;   // g_err is thread-local: carry the message back
-    rcs[s * kWorkers + k] = rc;
-    p2v_verifier_free(v);
-    if (st) (void)hipStreamDestroy(st);
+    const size_t m = b - a;
+    // one chunk: a verifier sized to the shard (64-proof granules, powers of two), else chunks
+    const size_t ch = m <= 64 ? m : auto_chunk(m, chunk);
+    size_t cap = 64;
+    while (cap < std::min(m, ch)) cap <<= 1;
+    if (m > ch) cap = ch;
+    HostPipe* p = nullptr;
+    int rc = pipe_acquire(c, devices[s], cap, &p);
+    if (rc == P2V_OK) {
+      rc = pipe_run(p, proofs + a * W, m, results + a, W, ch);
+      pipe_release(c, p, rc != P2V_OK);
+    }
+    if (rc != P2V_OK) msgs[s] = g_err;   // g_err is thread-local: carry the message back
+    rcs[s] = rc;
   };
-  std::vector<std::thread> pool;
+  if (shards == 1) work(0);   // the calling thread (a drop-in verifyProof call starts no thread)
+  else {
+    std::vector<std::thread> pool;
+    for (int s = 0; s < shards; s++) pool.emplace_back(work, s);
+    for (auto& t : pool) t.join();
+  }
   for (int s = 0; s < shards; s++)
-    for (int k = 0; k < kWorkers; k++) pool.emplace_back(work, s, k);
-  for (auto& t : pool) t.join();
-  for (int s = 0; s < shards * kWorkers; s++)
     if (rcs[s] != P2V_OK)
-      return fail(rcs[s], "shard " + std::to_string(s / kWorkers) + " (device " + std::to_string(devices[s / kWorkers]) + "): " + msgs[s]);
+      return fail(rcs[s], "shard " + std::to_string(s) + " (device " + std::to_string(devices[s]) + "): " + msgs[s]);
   return P2V_OK;
 }
 
@@ -977,6 +1137,25 @@ static int pack_json_into(p2v_verifier* v, const char* blob, const uint64_t* off
   return P2V_OK;
 }
 
+// the circuit's byte map (circuit.cpp bytes_map) on the verifier's device, made once
+static int ensure_bytes_map(p2v_verifier* v) {
+  if (v->have_bmap) return P2V_OK;
+  const BytesMap m = bytes_map(v->circ->c);
+  auto put = [&](DevBuf& b, const void* h, size_t bytes) -> hipError_t {
+    hipError_t e = b.alloc(bytes + 16);
+    if (e == hipSuccess && bytes) e = hipMemcpy(b.p, h, bytes, hipMemcpyHostToDevice);
+    return e;
+  };
+  HCK(put(v->b_rsrc, m.run_src.data(), m.run_src.size() * 8));
+  HCK(put(v->b_rdst, m.run_dst.data(), m.run_dst.size() * 8));
+  HCK(put(v->b_rlen, m.run_len.data(), m.run_len.size() * 8));
+  HCK(put(v->b_coff, m.chk_off.data(), m.chk_off.size() * 8));
+  HCK(put(v->b_cval, m.chk_val.data(), m.chk_val.size()));
+  v->nruns = (int)m.run_len.size(); v->nchk = (int)m.chk_off.size(); v->bfixed = m.fixed;
+  v->have_bmap = true;
+  return P2V_OK;
+}
+
 // plonky2 binary proofs -> packed rows of v->in (k_bytes_pack against the circuit's byte map,
 // the host reader for any proof that fails a check); codes[i] as p2v_pack_proof_bytes
 static int pack_bytes_into(p2v_verifier* v, const uint8_t* blob, const uint64_t* offsets, size_t n,
@@ -989,21 +1168,7 @@ static int pack_bytes_into(p2v_verifier* v, const uint8_t* blob, const uint64_t*
   hipStream_t st = (hipStream_t)stream_;
   const Circuit& C = v->circ->c;
   const int64_t W = C.L.words;
-  if (!v->have_bmap) {
-    const BytesMap m = bytes_map(C);
-    auto put = [&](DevBuf& b, const void* h, size_t bytes) -> hipError_t {
-      hipError_t e = b.alloc(bytes + 16);
-      if (e == hipSuccess && bytes) e = hipMemcpy(b.p, h, bytes, hipMemcpyHostToDevice);
-      return e;
-    };
-    HCK(put(v->b_rsrc, m.run_src.data(), m.run_src.size() * 8));
-    HCK(put(v->b_rdst, m.run_dst.data(), m.run_dst.size() * 8));
-    HCK(put(v->b_rlen, m.run_len.data(), m.run_len.size() * 8));
-    HCK(put(v->b_coff, m.chk_off.data(), m.chk_off.size() * 8));
-    HCK(put(v->b_cval, m.chk_val.data(), m.chk_val.size()));
-    v->nruns = (int)m.run_len.size(); v->nchk = (int)m.chk_off.size(); v->bfixed = m.fixed;
-    v->have_bmap = true;
-  }
+  { const int rc = ensure_bytes_map(v); if (rc != P2V_OK) return rc; }
   const uint64_t base = offsets[0], bytes = offsets[n] - base;
   if (v->j_blob.bytes < bytes + 64) { v->j_blob.free_(); HCK(v->j_blob.alloc(bytes + 64)); }   // + unaligned-load slack
   if (v->j_offs.bytes < (n + 1) * 8) { v->j_offs.free_(); HCK(v->j_offs.alloc((n + 1) * 8)); }
@@ -1032,6 +1197,113 @@ static int pack_bytes_into(p2v_verifier* v, const uint8_t* blob, const uint64_t*
     catch (...) { codes[i] = P2V_E_PARSE; }
   }
   return P2V_OK;
+}
+
+// plonky2 binary proofs in host memory, verified through the circuit's pooled pipe: per chunk the
+// bytes are copied on the copy stream, packed on the device (k_bytes_pack into a ring slot) and
+// verified on the compute stream, up to kRing chunks in flight.  Proofs the device packer flags
+// are packed by the host reader afterwards and verified in one more run (or get the reader's
+// code), so results and codes equal p2v_verifier_run_bytes'.
+int p2v_verify_batch_bytes(const p2v_circuit* c, const uint8_t* blob, const uint64_t* offsets, size_t n,
+                           int8_t* results, int32_t* codes, size_t* n_device, int device, size_t chunk) {
+  if (n_device) *n_device = 0;
+  if (!c || (n && (!blob || !offsets || !results || !codes))) return fail(P2V_E_ARG, "null argument");
+  if (n == 0) return P2V_OK;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(P2V_E_NODEVICE, "no HIP device available: libp2v verifies on MI355X only (no CPU fallback)");
+  if (device < 0 || device >= ndev) return fail(P2V_E_ARG, "bad device index");
+  const Circuit& C = c->c;
+  const size_t W = (size_t)C.L.words;
+  const size_t ch = auto_chunk(n, chunk);
+  size_t cap = 64;
+  while (cap < std::min(n, ch)) cap <<= 1;
+  if (n > ch) cap = ch;
+  HostPipe* p = nullptr;
+  int rc = pipe_acquire(c, device, cap, &p);
+  if (rc != P2V_OK) return rc;
+  auto body = [&]() -> int {
+    HCK(hipSetDevice(device));
+    { const int r = ensure_bytes_map(p->v); if (r != P2V_OK) return r; }
+    if (!p->have_ring) {
+      for (int k = 0; k < HostPipe::kRing; k++) {
+        HCK(p->ring[k].alloc(p->cap * W * 8));
+        HCK(hipEventCreateWithFlags(&p->copied[k], hipEventDisableTiming));
+        HCK(hipEventCreateWithFlags(&p->freed[k], hipEventDisableTiming));
+      }
+      p->have_ring = true;
+    }
+    if (p->dres.bytes < n) { p->dres.free_(); HCK(p->dres.alloc(n)); }
+    if (p->dok.bytes < n) { p->dok.free_(); HCK(p->dok.alloc(n)); }
+    if (p->h_res_cap < n) {
+      if (p->h_res) (void)hipHostFree(p->h_res);
+      p->h_res = nullptr; p->h_res_cap = 0;
+      HCK(hipHostMalloc((void**)&p->h_res, n));
+      p->h_res_cap = n;
+    }
+    if (p->h_ok_cap < n) {
+      if (p->h_ok) (void)hipHostFree(p->h_ok);
+      p->h_ok = nullptr; p->h_ok_cap = 0;
+      HCK(hipHostMalloc((void**)&p->h_ok, n));
+      p->h_ok_cap = n;
+    }
+    p2v_verifier* v = p->v;
+    const size_t nch = (n + ch - 1) / ch;
+    for (size_t i = 0; i < nch; i++) {
+      const int b = (int)(i % HostPipe::kRing);
+      const size_t off = i * ch, len = std::min(ch, n - off);
+      const uint64_t base = offsets[off], bytes = offsets[off + len] - base;
+      if (i >= (size_t)HostPipe::kRing) {
+        HCK(hipEventSynchronize(p->copied[b]));              // the slot's host offsets are no longer read
+        HCK(hipStreamWaitEvent(p->cs, p->freed[b], 0));      // its device buffers' last reader is done
+      }
+      if (p->bbytes[b].bytes < bytes + 64) { p->bbytes[b].free_(); HCK(p->bbytes[b].alloc(bytes + 64)); }   // + unaligned-load slack
+      if (p->boffs[b].bytes < (len + 1) * 8) { p->boffs[b].free_(); HCK(p->boffs[b].alloc((p->cap + 1) * 8)); }
+      auto& ho = p->hoffs[b];
+      ho.resize(len + 1);
+      for (size_t k = 0; k <= len; k++) ho[k] = offsets[off + k] - base;
+      HCK(hipMemcpyAsync(p->bbytes[b].p, blob + base, bytes, hipMemcpyHostToDevice, p->cs));
+      HCK(hipMemcpyAsync(p->boffs[b].p, ho.data(), (len + 1) * 8, hipMemcpyHostToDevice, p->cs));
+      HCK(hipEventRecord(p->copied[b], p->cs));
+      HCK(hipStreamWaitEvent(p->st, p->copied[b], 0));
+      k_bytes_pack<<<(unsigned)len, 256, 0, p->st>>>((const uint8_t*)p->bbytes[b].p, (const uint64_t*)p->boffs[b].p, (int)len,
+                                                      (const int64_t*)v->b_rsrc.p, (const int64_t*)v->b_rdst.p, (const int64_t*)v->b_rlen.p,
+                                                      v->nruns, (const int64_t*)v->b_coff.p, (const uint8_t*)v->b_cval.p, v->nchk, v->bfixed,
+                                                      (int64_t)C.num_pis, C.L.pis, (uint64_t*)p->ring[b].p, (int64_t)W,
+                                                      (int8_t*)p->dok.p + off);
+      HCK(hipGetLastError());
+      const int r = p2v_verifier_run(v, (const uint64_t*)p->ring[b].p, len, (int8_t*)p->dres.p + off, nullptr, p->st,
+                                     P2V_FLAG_INPUT_DEVICE | P2V_FLAG_RESULT_DEVICE | P2V_FLAG_NO_SYNC);
+      if (r != P2V_OK) return r;
+      HCK(hipEventRecord(p->freed[b], p->st));
+    }
+    HCK(hipMemcpyAsync(p->h_res, p->dres.p, n, hipMemcpyDeviceToHost, p->st));
+    HCK(hipMemcpyAsync(p->h_ok, p->dok.p, n, hipMemcpyDeviceToHost, p->st));
+    HCK(hipStreamSynchronize(p->st));
+    memcpy(results, p->h_res, n);
+    // the proofs the device packer did not take: the host reader, then one more run for those it packs
+    std::vector<size_t> redo;
+    std::vector<uint64_t> rows;
+    for (size_t i = 0; i < n; i++) {
+      codes[i] = P2V_OK;
+      if (p->h_ok[i]) { if (n_device) (*n_device)++; continue; }
+      rows.resize((redo.size() + 1) * W);
+      try {
+        pack_proof_bytes(C, blob + offsets[i], (size_t)(offsets[i + 1] - offsets[i]), rows.data() + redo.size() * W);
+        redo.push_back(i);
+      } catch (const ShapeError&) { codes[i] = P2V_E_SHAPE; results[i] = P2V_ERR_SHAPE; }
+      catch (...) { codes[i] = P2V_E_PARSE; results[i] = P2V_ERR_PARSE; }
+    }
+    if (!redo.empty()) {
+      std::vector<int8_t> rr(redo.size());
+      const int r = pipe_run(p, rows.data(), redo.size(), rr.data(), W, p->cap);
+      if (r != P2V_OK) return r;
+      for (size_t k = 0; k < redo.size(); k++) results[redo[k]] = rr[k];
+    }
+    return P2V_OK;
+  };
+  rc = body();
+  pipe_release(c, p, rc != P2V_OK);
+  return rc;
 }
 
 int p2v_verifier_pack_bytes(p2v_verifier* v, const uint8_t* blob, const uint64_t* offsets, size_t n,
@@ -1085,30 +1357,54 @@ int p2v_verifier_run_json(p2v_verifier* v, const char* blob, const uint64_t* off
 }
 
 int p2v_selftest(int device, int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n) {
-  if (op < 0 || op > 4 || (n && (!a || !out || ((op == 0 || op == 3 || op == 4) && !b)))) return fail(P2V_E_ARG, "bad op / null argument");
+  const bool needs_b = op == 0 || op == 3 || op == 4 || op == 6;
+  if (op < 0 || op > 11 || (n && (!a || !out || (needs_b && !b)))) return fail(P2V_E_ARG, "bad op / null argument");
   const int ndev = p2v_device_count();
   if (ndev == 0) return fail(P2V_E_NODEVICE, "no HIP device");
   if (device < 0 || device >= ndev) return fail(P2V_E_ARG, "bad device index");
   if (n == 0) return P2V_OK;
   HCK(hipSetDevice(device));
-  const bool fm = op == 0 || op == 3;
-  const size_t w = fm ? 1 : 12;
+  // words per item of a / b and of out
+  const bool scalar = op == 0 || op == 3 || op == 5 || op == 6 || op == 7 || op == 8;
+  const size_t w = scalar ? 1 : 12, wo = op == 6 ? 2 : w;
+  const size_t bw = op == 4 ? 24 : scalar && needs_b ? n : 2;
   DevBuf da, db, dout;
   auto cleanup = [&]() { da.free_(); db.free_(); dout.free_(); };
   hipError_t e = da.alloc(n * w * 8);
-  if (e == hipSuccess) e = db.alloc(fm ? n * 8 : op == 4 ? 24 * 8 : 16);
-  if (e == hipSuccess) e = dout.alloc(n * w * 8);
+  if (e == hipSuccess) e = db.alloc(bw * 8);
+  if (e == hipSuccess) e = dout.alloc(n * wo * 8);
   if (e == hipSuccess) e = hipMemcpy(da.p, a, n * w * 8, hipMemcpyHostToDevice);
-  if (e == hipSuccess && fm) e = hipMemcpy(db.p, b, n * 8, hipMemcpyHostToDevice);
-  if (e == hipSuccess && op == 4) e = hipMemcpy(db.p, b, 24 * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess && needs_b) e = hipMemcpy(db.p, b, bw * 8, hipMemcpyHostToDevice);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(k_selftest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, op, (const uint64_t*)da.p,
-                       (const uint64_t*)db.p, (uint64_t*)dout.p, (int64_t)n);
+    if (op >= 9) {
+      const int lanes = op == 9 ? 16 : op == 10 ? 4 : 2;
+      hipLaunchKernelGGL(k_selftest_forms, dim3((unsigned)((n * lanes + 255) / 256)), dim3(256), 0, 0, op, (const uint64_t*)da.p,
+                         (uint64_t*)dout.p, (int64_t)n);
+    } else {
+      hipLaunchKernelGGL(k_selftest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, op, (const uint64_t*)da.p,
+                         (const uint64_t*)db.p, (uint64_t*)dout.p, (int64_t)n);
+    }
     e = hipGetLastError();
   }
-  if (e == hipSuccess) e = hipMemcpy(out, dout.p, n * w * 8, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(out, dout.p, n * wo * 8, hipMemcpyDeviceToHost);
   cleanup();
   if (e != hipSuccess) return fail(P2V_E_DEVICE, std::string("p2v_selftest: ") + hipGetErrorString(e));
+  return P2V_OK;
+}
+
+int p2v_count_mismatches(const int8_t* results, const int8_t* expect, size_t n, uint64_t* counters, void* stream) {
+  if (!counters || (n && (!results || !expect))) return fail(P2V_E_ARG, "null argument");
+  const unsigned blocks = n ? (unsigned)((n + 255) / 256) : 1;
+  hipLaunchKernelGGL(k_count_mismatches, dim3(blocks), dim3(256), 0, (hipStream_t)stream, results, expect, (int64_t)n,
+                     (unsigned long long*)counters);
+  HCK(hipGetLastError());
+  return P2V_OK;
+}
+
+int p2v_clock_probe(uint64_t* stamps, int nblocks, void* stream) {
+  if (!stamps || nblocks <= 0) return fail(P2V_E_ARG, "null argument / no blocks");
+  hipLaunchKernelGGL(k_clock_probe, dim3((unsigned)nblocks), dim3(64), 0, (hipStream_t)stream, (unsigned long long*)stamps);
+  HCK(hipGetLastError());
   return P2V_OK;
 }
 
@@ -1120,12 +1416,8 @@ int p2v_verifier_last_timings(const p2v_verifier* v, float* out, int max) {
 }
 
 int p2v_verify_batch(const p2v_circuit* c, const uint64_t* proofs, size_t n, int8_t* results, int device) {
-  p2v_verifier* v = nullptr;
-  int rc = p2v_verifier_create(c, device, n ? n : 1, &v);
-  if (rc != P2V_OK) return rc;
-  rc = p2v_verifier_run(v, proofs, n, results, nullptr, nullptr, 0);
-  p2v_verifier_free(v);
-  return rc;
+  if (!c || (n && (!proofs || !results))) return fail(P2V_E_ARG, "null argument");
+  return p2v_verify_batch_devices(c, proofs, n, results, &device, 1, 0);
 }
 
 }  // extern "C"

@@ -293,8 +293,8 @@ __device__ __forceinline__ void transcript_quad(const DevCircuit& c, int p, int 
 }
 
 // Lane form of the same transcript: one lane per proof, the whole state in its registers, the
-// throughput permutation (p2::permute_dev).  A third of the quad form's VALU instructions per
-// proof, but a chain ~3.5x longer (a lone wave issues its dependent permutation at its own
+// throughput permutation (p2::permute_dev).  About half of the quad form's VALU instructions per
+// proof (85.9 M against 169.4 M per 4096 proofs), but a chain ~3.5x longer (a lone wave issues its dependent permutation at its own
 // latency): for pipelines with enough batches in flight to hide it (round 4, P2V_TRANSCRIPT=lane).
 __device__ __forceinline__ void transcript_lane(const DevCircuit& c, int p) {
   uint64_t x[12];
@@ -882,10 +882,21 @@ extern "C" __global__ void __launch_bounds__(256) k_status(DevCircuit c, int8_t*
 // op 2 the 2-to-1 compression form (permute_dev(s, zh, gm = words 0..3), Hash/Merkle.hs:21-24;
 // a = n states whose words 8..11 are ignored and taken as 0), op 4 one MDS layer + constants
 // (the permutation's row reduction with its grouped carry fix-up).  One lane per item.
+// ops 5-8: the S-box forms x -> x^7 (Hash/Poseidon.hs:92-96) with their rare -2^64 fix-ups
+// (ADVICE r4): 5 sbox_n<1> (throughput permutation, partial rounds), 6 sbox_n<2> on the pair
+// (a[i], b[i]) (full rounds; out[2i], out[2i+1]), 7 sbox_lat_br (row form), 8 sbox_lat (quad /
+// pair forms); canonical outputs.
 extern "C" __global__ void __launch_bounds__(256) k_selftest(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  if (op == 0) {
+  if (op >= 5 && op <= 8) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (op == 5) { uint64_t x = a[i]; p2::dv::sbox_n<1>(&x); out[i] = gl::canon(x); }
+    else if (op == 6) { uint64_t x[2] = {a[i], b[i]}; p2::dv::sbox_n<2>(x); out[2 * i] = gl::canon(x[0]); out[2 * i + 1] = gl::canon(x[1]); }
+    else if (op == 7) out[i] = gl::canon(p2::sbox_lat_br(a[i]));
+    else out[i] = gl::canon(p2::sbox_lat(a[i]));
+#endif
+  } else if (op == 0) {
     out[i] = gl::mul(a[i], b[i]);
   } else if (op == 3) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -917,5 +928,39 @@ extern "C" __global__ void __launch_bounds__(256) k_selftest(int op, const uint6
     else p2::permute_dev(s, true, 1);
 #pragma unroll
     for (int k = 0; k < 12; k++) out[12 * i + k] = op == 2 && k >= 4 ? 0 : s[k];
+  }
+}
+
+// The latency forms of the permutation on caller-chosen states (p2v_selftest ops 9-11; ADVICE
+// r4): 9 the row form (rposeidon.h, 16 lanes per state), 10 the quad form (qposeidon.h, 4 lanes),
+// 11 the pair form (pposeidon.h, 2 lanes).  Every lane of a group takes part in the DPP moves, so
+// lanes past n compute on a copy of state n - 1 and store nothing.  a, out: n states of 12 words.
+extern "C" __global__ void __launch_bounds__(256) k_selftest_forms(int op, const uint64_t* a, uint64_t* out, int64_t n) {
+  __shared__ TLdsAny T;
+  if (op == 11) pp::tlds_fill(T.p, threadIdx.x, 256);
+  else qp::tlds_fill(T.q, threadIdx.x, 256);
+  const int lanes = op == 9 ? 16 : op == 10 ? 4 : 2;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t item = g / lanes, src = item < n ? item : n - 1;
+  const int t = (int)(g % lanes);
+  const uint64_t* s = a + 12 * src;
+  uint64_t* o = out + 12 * item;
+  if (op == 9) {
+    rp::Row R;
+    rp::init(R, threadIdx.x);
+    const uint64_t x = rp::permute(R.L < 12 ? s[R.L] : 0, R, T.q);
+    if (item < n && R.L < 12) o[R.L] = x;
+  } else if (op == 10) {
+    uint64_t x[3] = {s[3 * t], s[3 * t + 1], s[3 * t + 2]};
+    qp::permute(x, t, T.q);
+    if (item < n) for (int k = 0; k < 3; k++) o[3 * t + k] = x[k];
+  } else {
+    uint64_t x[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) x[k] = s[6 * t + k];
+    pp::permute(x, t, T.p);
+    if (item < n)
+#pragma unroll
+      for (int k = 0; k < 6; k++) o[6 * t + k] = x[k];
   }
 }

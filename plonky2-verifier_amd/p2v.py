@@ -67,6 +67,7 @@ FLAG_NO_SYNC = 4
 FLAG_UNIT_FILTERS = 8   # parity mode (tests only): every gate filter / lookup selector := 1
 FLAG_INPUT_TILED = 16   # the batch in 64-proof tiles [n/64][words][64] (tile_proofs)
 FLAG_LOOKAHEAD = 32     # the device batch is complete at the call: its transcript may run ahead (include/p2v.h)
+SHAPE_LIMIT = 1 << 20   # public inputs / final-polynomial coefficients a shape variant may hold (include/p2v.h)
 
 
 class P2VError(RuntimeError):
@@ -136,8 +137,11 @@ def lib() -> ctypes.CDLL:
     L.p2v_verifier_pack_bytes.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp]
     L.p2v_verify_batch.argtypes = [vp, u64p, sz, i8p, ctypes.c_int]
     L.p2v_verify_batch_devices.argtypes = [vp, u64p, sz, i8p, ctypes.POINTER(ctypes.c_int), ctypes.c_int, sz]
+    L.p2v_verify_batch_bytes.argtypes = [vp, vp, vp, sz, i8p, vp, vp, ctypes.c_int, sz]
     L.p2v_verifier_last_timings.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
     L.p2v_selftest.argtypes = [ctypes.c_int, ctypes.c_int, u64p, u64p, u64p, sz]
+    L.p2v_count_mismatches.argtypes = [i8p, i8p, sz, u64p, vp]
+    L.p2v_clock_probe.argtypes = [u64p, ctypes.c_int, vp]
     L.p2v_proof_shape_json.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
     L.p2v_proof_shape_words.argtypes = [u64p, sz, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
     L.p2v_circuit_shape_variant.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp)]
@@ -557,15 +561,48 @@ def _status_to_bool(st: int) -> bool:
 
 
 def device_selftest(op: int, a: np.ndarray, b: Optional[np.ndarray] = None, device: int = 0) -> np.ndarray:
-    """p2v_selftest: the device field multiply (op 0, a * b mod p; op 3 the S-box's form), Poseidon permutation (op 1,
-    a = [n, 12] states) or 2-to-1 compression form (op 2, words 8..11 taken as 0, words 0..3
-    returned) on `device`."""
+    """p2v_selftest (include/p2v.h): the device field multiply (op 0, a * b mod p; op 3 the S-box's
+    form), Poseidon permutation (op 1, a = [n, 12] states), 2-to-1 compression form (op 2, words
+    8..11 taken as 0, words 0..3 returned), one MDS layer (op 4), the S-box forms (ops 5-8, x^7;
+    op 6 the grouped pair (a[i], b[i]) -> out [n, 2]) and the latency forms of the permutation
+    (ops 9-11: row, quad, pair) on `device`."""
     a = np.ascontiguousarray(a, dtype=np.uint64)
     n = a.shape[0]
-    out = np.zeros_like(a)   # op 4: one MDS layer + constants b = [kl[12], kh[12]] (include/p2v.h)
+    out = np.zeros((n, 2), dtype=np.uint64) if op == 6 else np.zeros_like(a)   # op 4: b = [kl[12], kh[12]]
     bb = np.ascontiguousarray(b, dtype=np.uint64) if b is not None else None
     _check(lib().p2v_selftest(device, op, a.ctypes.data, bb.ctypes.data if bb is not None else None, out.ctypes.data, n))
     return out
+
+
+def count_mismatches(results_ptr: int, expect_ptr: int, n: int, counters_ptr: int, stream: int = 0) -> None:
+    """p2v_count_mismatches (device pointers, enqueued on `stream`): counters[0] += #{results !=
+    expect}, counters[1] += 1.  The bench folds every timed launch's statuses into it."""
+    _check(lib().p2v_count_mismatches(ctypes.c_void_p(results_ptr), ctypes.c_void_p(expect_ptr), n,
+                                      ctypes.c_void_p(counters_ptr), ctypes.c_void_p(stream)))
+
+
+def clock_probe(stamps_ptr: int, nblocks: int, stream: int = 0) -> None:
+    """p2v_clock_probe: nblocks one-wave workgroups write (XCC id, s_memtime, s_memrealtime) to
+    the device buffer stamps[3 * nblocks] (u64), on `stream`."""
+    _check(lib().p2v_clock_probe(ctypes.c_void_p(stamps_ptr), nblocks, ctypes.c_void_p(stream)))
+
+
+def clock_from_probes(start: np.ndarray, end: np.ndarray) -> Optional[dict]:
+    """The shader clock over the interval between two clock_probe launches: per XCD, the median
+    stamp of each probe, d(s_memtime) / d(s_memrealtime) x 100 MHz (MI355X_MICROARCH.md, DVFS
+    item 6).  start / end: [nblocks, 3] u64 stamps."""
+    per = {}
+    for x in sorted(set(int(v) for v in start[:, 0]) & set(int(v) for v in end[:, 0])):
+        a, b = start[start[:, 0] == x], end[end[:, 0] == x]
+        dt = float(np.median(b[:, 1].astype(np.float64))) - float(np.median(a[:, 1].astype(np.float64)))
+        dr = float(np.median(b[:, 2].astype(np.float64))) - float(np.median(a[:, 2].astype(np.float64)))
+        if dr > 0:
+            per[x] = dt / dr * 0.1   # GHz: memrealtime counts at 100 MHz
+    if not per:
+        return None
+    v = list(per.values())
+    return {"clock_ghz": round(float(np.mean(v)), 4), "min_ghz": round(min(v), 4), "max_ghz": round(max(v), 4),
+            "xcds": len(per), "interval_ms": round(dr / 1e5, 3)}
 
 
 def verify_proof(vkey: VerifierCircuitData, proof: Union[ProofWithPublicInputs, str, bytes], device: int = 0) -> bool:
@@ -573,9 +610,17 @@ def verify_proof(vkey: VerifierCircuitData, proof: Union[ProofWithPublicInputs, 
     reference raises `error`.  Public inputs and the final polynomial are taken at the length
     the proof carries (a shape variant of the circuit when it differs, as the reference does)."""
     text = proof.json if isinstance(proof, ProofWithPublicInputs) else _bytes(proof)
-    vk = vkey.for_proof(text)
-    packed = vk.pack(text)[None, :]
+    vk = vkey
+    packed = np.empty((1, vkey.info.proof_words), dtype=np.uint64)
+    rc = lib().p2v_pack_proof_json(vkey.handle, text, len(text), packed.ctypes.data)
+    if rc == E_SHAPE:   # other public-input / final-polynomial lengths: the circuit's shape variant
+        vk = vkey.for_proof(text)
+        packed = vk.pack(text)[None, :]
+    else:
+        _check(rc)
     res = np.empty(1, dtype=np.int8)
+    # libp2v keeps the circuit's verifier between calls (p2v_verify_batch's pool), so a repeated
+    # call costs the kernels, not a workspace
     _check(lib().p2v_verify_batch(vk.handle, packed.ctypes.data, 1, res.ctypes.data, device))
     return _status_to_bool(int(res[0]))
 
@@ -609,9 +654,16 @@ def verify_proof_batch(vkey: VerifierCircuitData, proofs: Iterable[Union[ProofWi
             vk = vkey.for_proof(texts[i])
         except P2VError:
             # lengths past this build's limits (include/p2v.h, 2^20): the transcript cannot match
-            # the circuit's, so the reference's answer is False (barring a PoW collision)
-            res[i] = REJECT
-            continue
+            # the circuit's, so the reference's answer is False (barring a PoW collision).  Any
+            # other shape-variant failure (a circuit that does not validate, allocation) is an
+            # error, not a verdict
+            npi, nf = ctypes.c_int(), ctypes.c_int()
+            b = texts[i]
+            if (lib().p2v_proof_shape_json(b, len(b), ctypes.byref(npi), ctypes.byref(nf)) == E_OK
+                    and (npi.value > SHAPE_LIMIT or nf.value > SHAPE_LIMIT)):
+                res[i] = REJECT
+                continue
+            raise
         if vk is vkey:   # another list-length mismatch: an `error` in the reference as well
             raise P2VError(E_SHAPE, f"proof {i}: " + _pack_error(vkey, texts[i]))
         groups.setdefault(id(vk), (vk, []))[1].append(int(i))
@@ -642,6 +694,30 @@ def verify_batch_devices(vkey: VerifierCircuitData, packed: np.ndarray, devices:
     devs = (ctypes.c_int * len(devices))(*devices)
     _check(lib().p2v_verify_batch_devices(vkey.handle, packed.ctypes.data, n, res.ctypes.data, devs, len(devices), chunk))
     return res
+
+
+def verify_batch(vkey: VerifierCircuitData, packed: np.ndarray, device: int = 0) -> np.ndarray:
+    """p2v_verify_batch: packed rows [n, proof_words] in host memory (pinned for the full link
+    rate), verified by the circuit's pooled verifier on `device`, H2D copies overlapped with the
+    verification in chunks; int8 statuses."""
+    packed = np.ascontiguousarray(packed, dtype=np.uint64)
+    n = packed.shape[0]
+    res = np.empty(n, dtype=np.int8)
+    _check(lib().p2v_verify_batch(vkey.handle, packed.ctypes.data, n, res.ctypes.data, device))
+    return res
+
+
+def verify_batch_bytes(vkey: VerifierCircuitData, proofs: Union[Sequence[bytes], tuple], device: int = 0, chunk: int = 0):
+    """p2v_verify_batch_bytes: plonky2 binary proofs (a list, or a (uint8 blob, uint64 offsets[n+1])
+    pair, e.g. in pinned memory) -> (int8 statuses, int32 decode codes, proofs the device packed)."""
+    blob, offs = BatchVerifier._json_batch(proofs)
+    n = offs.size - 1
+    res = np.empty(n, dtype=np.int8)
+    codes = np.empty(n, dtype=np.int32)
+    ndev = ctypes.c_size_t(0)
+    _check(lib().p2v_verify_batch_bytes(vkey.handle, blob.ctypes.data, offs.ctypes.data, n, res.ctypes.data, codes.ctypes.data,
+                                        ctypes.addressof(ndev), device, chunk))
+    return res, codes, ndev.value
 
 
 def shard_bounds(n: int, world: int, rank: int):

@@ -140,3 +140,39 @@ def test_bench_max_over_ranks_on_gloo_side_group():
         p.join(timeout=120)
         assert p.exitcode == 0
     assert [v for _, v in res] == [2.5, 2.5, 2.5]
+
+
+def _worker_per_rank(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    grp = dist.new_group(backend="gloo")
+    # rank r verified 4096 proofs in (1 + r) seconds at a shader clock of 2.0 + 0.1 r GHz
+    summ = bench.per_rank_summary(4096, 1.0 + rank, world, grp, clock_ghz=2.0 + 0.1 * rank)
+    out.put((rank, summ, bench.gather_over_ranks(float(rank), world, grp)))
+    dist.barrier(group=grp)
+    dist.destroy_process_group()
+
+
+def test_bench_per_rank_summary_on_gloo_side_group():
+    """the bench reports every rank's own throughput (its proofs over its own
+    time before the closing barrier), min / max, the imbalance and every rank's shader clock, all
+    gathered over the gloo side group; every rank holds the same summary, in rank order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_per_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in range(2)), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, summ, ranks in res:
+        assert ranks == [0.0, 1.0]
+        assert summ["proofs_per_s"] == [4096.0, 2048.0]
+        assert summ["min"] == 2048.0 and summ["max"] == 4096.0
+        assert summ["imbalance"] == 0.5
+        assert summ["clock_ghz"] == [2.0, 2.1]

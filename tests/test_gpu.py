@@ -611,6 +611,69 @@ def test_gpu_multi_device_entry_point(p2v):
         p2v.verify_batch_devices(vk, arr, [0, 99])
 
 
+def test_gpu_verify_batch_pool_reuse_and_chunks(p2v):
+    """p2v_verify_batch keeps the circuit's verifier between calls and
+    streams larger batches in chunks (H2D on a copy stream, three chunk buffers in flight).  One
+    circuit handle, calls of 1, 64, 65, 700 (chunks of 256: three chunks, the ring wraps) and 3000
+    proofs in varying order (from pageable and from pinned host memory), several threads at once:
+    every call equals the single-workspace statuses."""
+    import threading
+    import torch
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    pool = vk.pack_many([gc.proof(1, 1), gc.proof(1, 5, flags=2), gc.proof(1, 4, flags=1), gc.proof(2, 2)])
+    idx = np.random.default_rng(5).integers(0, 4, 3000)
+    arr = np.ascontiguousarray(pool[idx])
+    want = p2v.BatchVerifier(vk, 0, len(idx)).run(arr)
+    assert sorted(set(want.tolist())) == [-3, 0, 1]
+    pinned = torch.from_numpy(arr.view(np.int64)).pin_memory().numpy().view(np.uint64)
+    for n in (1, 64, 65, 700, 1, 3000, 64, 2):
+        src = pinned if n % 2 else arr
+        assert np.array_equal(p2v.verify_batch(vk, src[:n]), want[:n]), n
+    got = p2v.verify_batch_devices(vk, arr[:700], [0], chunk=256)
+    assert np.array_equal(got, want[:700])
+    errs = []
+
+    def worker(k):
+        try:
+            for n in (1 + k, 300 + 7 * k, 64):
+                if not np.array_equal(p2v.verify_batch(vk, arr[k:k + n]), want[k:k + n]):
+                    errs.append((k, n))
+        except Exception as e:   # noqa: BLE001
+            errs.append((k, repr(e)))
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+    assert p2v.verify_proof(vk, gc.proof(1, 1)) is True
+    assert p2v.verify_proof(vk, gc.proof(1, 5, flags=2)) is False
+
+
+def test_gpu_verify_batch_bytes_pipelined(p2v):
+    """p2v_verify_batch_bytes (chunked copies, device packing and verification overlapped) equals
+    p2v_verifier_run_bytes on a batch with malformed proofs spread over several chunks: statuses,
+    decode codes and the device-packed count."""
+    from support import proof_bytes
+    gc = gen_circuit(6, 4, 0)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    texts = [gc.proof(1, 1), gc.proof(2, 2), gc.proof(1, 3, flags=1), gc.proof(1, 4, flags=2)]
+    bins = [proof_bytes(t, pi_prefix=bool(i % 2)) for i, t in enumerate(texts)]
+    bad = [bins[0][: len(bins[0]) // 3], bins[1] + b"\0" * 8]
+    batch = [bins[i % 4] for i in range(1100)]
+    for k in (5, 400, 777, 1099):
+        batch[k] = bad[k % 2]
+    bv = p2v.BatchVerifier(vk, 0, len(batch))
+    res_ref, codes_ref = bv.run_bytes(batch)
+    ndev_ref = bv.last_bytes_device
+    for chunk in (0, 256, 5000):
+        res, codes, ndev = p2v.verify_batch_bytes(vk, batch, 0, chunk)
+        assert np.array_equal(codes, codes_ref), chunk
+        assert np.array_equal(res, res_ref), chunk
+        assert ndev == ndev_ref == len(batch) - 4
+
+
 def test_gpu_multi_device_distinct_devices(p2v):
     """p2v_verify_batch_devices over distinct GPUs (all visible, up to 8): each shard on its own
     device must give the single-verifier statuses.  Needs >= 2 GPUs (the driver's multi-GPU
@@ -1038,6 +1101,48 @@ def test_gpu_mds_layer_carry_fixup(p2v):
             assert int(o[i]) % P == (al + (ah << 32)) % P, (i, s)
             fired += ((al + (ah >> 32) * 0xFFFFFFFF) >> 32) + (ah & 0xFFFFFFFF) >= 1 << 32   # the carry of reduce_rows
     assert fired > 300   # the fix-up branch really ran (hundreds of rows, in every group)
+
+
+def test_gpu_sbox_forms_edge_values(p2v):
+    """every S-box form (the throughput permutation's single and grouped S-boxes, the row
+    form's, the quad / pair forms') against x^7 mod p on the inputs whose products take the device
+    multiply's rare -2^64 fix-up (2^48 -> 2^96, ...): 2^k, 2^k +- 1, p - 2^k, p - 1, in lanes
+    mixed with random values, so the wave-uniform fix-up branch runs with some lanes needing it and
+    others not."""
+    from support import sbox_edge_values
+    ev = sbox_edge_values()
+    rng = np.random.default_rng(17)
+    rnd = [int(x) for x in rng.integers(0, 1 << 64, size=3 * len(ev), dtype=np.uint64)]
+    xs = ev + rnd + ev[::-1]
+    rng.shuffle(xs)
+    a = np.array(xs, dtype=np.uint64)
+    exp = np.array([pow(x % P, 7, P) for x in xs], dtype=np.uint64)
+    for op in (5, 7, 8):
+        out = p2v.device_selftest(op, a)
+        bad = np.nonzero(out != exp)[0]
+        assert len(bad) == 0, [(op, hex(int(a[i])), hex(int(out[i])), hex(int(exp[i]))) for i in bad[:5]]
+    b = a[::-1].copy()
+    out = p2v.device_selftest(6, a, b)
+    assert np.array_equal(out[:, 0], exp) and np.array_equal(out[:, 1], exp[::-1])
+
+
+def test_gpu_permutation_forms_first_round_wrap(p2v):
+    """states whose round-0 S-box inputs are exactly the wrap-taking edge values (state
+    word = edge value - rc0[i], so state + rc0 = 2^48, ...), plus the KAT and random states, through
+    the throughput permutation (op 1) and the transcript / small-batch latency forms (row, quad,
+    pair: ops 9-11), against the oracle's permutation (Hash/Poseidon.hs:42-46)."""
+    from support import KAT_IN, KAT_OUT, first_round_wrap_states
+    O = oracle()
+    rng = np.random.default_rng(23)
+    states = [KAT_IN] + first_round_wrap_states(n_extra=200)
+    states += [[int(x) for x in row] for row in rng.integers(0, 1 << 64, size=(300, 12), dtype=np.uint64)]
+    a = np.array(states, dtype=np.uint64)
+    exp = np.array([O.permute([int(x) % P for x in st]) for st in states], dtype=np.uint64)
+    assert [int(x) for x in exp[0]] == KAT_OUT
+    for op in (1, 9, 10, 11):
+        out = p2v.device_selftest(op, a)
+        bad = np.nonzero((out != exp).any(axis=1))[0]
+        assert len(bad) == 0, (op, [int(i) for i in bad[:5]])
 
 
 def test_gpu_latency_and_batch_modes_interleaved(p2v):

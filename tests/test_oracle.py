@@ -188,3 +188,24 @@ def test_coset_gate_matches_reference_example():
     assert oracle().L.or_gate_kind(gates[0].encode()) == oracle().L.or_gate_kind(
         b"CosetInterpolationGate { subgroup_bits: 4, degree: 6, barycentric_weights: [17293822565076172801], "
         b"_phantom: PhantomData<plonky2_field::goldilocks_field::GoldilocksField> }<D=2>")
+
+
+def test_first_round_wrap_states_hit_their_targets():
+    """The crafted permutation states of the GPU S-box tests: round 0's constant addition (as
+    p2::add_nc computes it) lands exactly on the S-box edge value, except where no 64-bit word
+    can (then on the congruent y + p)."""
+    from support import EPS, add_nc, first_round_wrap_states, preimage_round0, round0_constants, sbox_edge_values
+    rc0 = round0_constants()
+    exact = 0
+    for y in sbox_edge_values():
+        for i in range(12):
+            w = preimage_round0(y, i, rc0)
+            assert 0 <= w < 1 << 64
+            got = add_nc(w, rc0[i])
+            assert got % P == y % P
+            exact += got == y
+            if y >= rc0[i] or y >= EPS:
+                assert got == y
+    assert exact > 0.6 * 12 * len(sbox_edge_values())   # y < min(rc0[i], 2^32 - 1): no 64-bit word reaches y itself
+    st = first_round_wrap_states()
+    assert any(add_nc(w, rc0[i]) == 1 << 48 for s in st for i, w in enumerate(s))
