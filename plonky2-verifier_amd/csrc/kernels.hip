@@ -20,6 +20,7 @@
 #include "qposeidon.h"
 #include "rposeidon.h"
 #include "pposeidon.h"
+#include "lposeidon.h"
 
 using namespace p2d;
 using gl::E;
@@ -126,14 +127,27 @@ __device__ __forceinline__ E horner_strided(const DevCircuit& c, int64_t off, in
   return h;
 }
 
-__device__ __forceinline__ void transcript_row(const DevCircuit& c, int p, const rp::Row& R, const qp::TLds& T) {
+// the row form's permutation: lposeidon.h (round 5: LDS exchange, merged partial blocks; 8.1-8.6 us
+// per dependent permutation against 11.7-12.3 us for the DPP form of rposeidon.h,
+// profiles/r05e_lrow_chain.txt); P2V_ROW_LAT=0 rebuilds the DPP form
+#ifndef P2V_ROW_LAT
+#define P2V_ROW_LAT 1
+#endif
+#if P2V_ROW_LAT
+#define ROW_PERMUTE(x) lp::permute((x), LR, TL)
+#else
+#define ROW_PERMUTE(x) rp::permute((x), R, TQ)
+#endif
+__device__ __forceinline__ void transcript_row(const DevCircuit& c, int p, const rp::Row& R, const lp::Row& LR, const qp::TLds& TQ,
+                                               const lp::TLdsL& TL) {
+  (void)LR; (void)TQ; (void)TL;
   const int L = R.L;
   // public inputs hash, Hash/Sponge.hs:26-31 (sponge [] = zero digest)
   uint64_t x = 0;
   for (int i = 0; i < c.num_pis; i += 8) {
     const int k = c.num_pis - i;
     if (L < 8 && L < k) x = ld(c, c.pis + i + L, p);
-    x = rp::permute(x, R, T);
+    x = ROW_PERMUTE(x);
   }
   uint64_t pih[4];
 #pragma unroll
@@ -167,7 +181,7 @@ __device__ __forceinline__ void transcript_row(const DevCircuit& c, int p, const
         if (type == TOP_ABSORB_SOA) { if (mine) v = ld(c, (int64_t)a + j, p); }
         else if (type == TOP_ABSORB_PIH) { const int w = j & 3; v = w == 0 ? pih[0] : w == 1 ? pih[1] : w == 2 ? pih[2] : pih[3]; }
         else v = c.digest[j & 3];
-        if (nbuf == 8) { x = rp::permute(x, R, T); nbuf = 0; }   // overwrite mode: the rate part is replaced
+        if (nbuf == 8) { x = ROW_PERMUTE(x); nbuf = 0; }   // overwrite mode: the rate part is replaced
         if (mine) x = v;
         nbuf += take;
         k += take;
@@ -175,7 +189,7 @@ __device__ __forceinline__ void transcript_row(const DevCircuit& c, int p, const
       continue;
     }
     for (int k = 0; k < n; k++) {   // squeeze: output order state[7], state[6], ... (reverse of take 8)
-      if (absorbing || outpos < 0) { x = rp::permute(x, R, T); absorbing = false; outpos = 7; }
+      if (absorbing || outpos < 0) { x = ROW_PERMUTE(x); absorbing = false; outpos = 7; }
       uint64_t w = rp::get_word(x, outpos);
       outpos--;
       if (type == TOP_SQUEEZE_IDX) w &= qmask;
@@ -451,13 +465,13 @@ __device__ __forceinline__ void transcript_pair(const DevCircuit& c, int p, int 
 }
 
 // the constant tables of the transcript forms, in LDS (qposeidon.h TLds, pposeidon.h TLdsP)
-union TLdsAny { qp::TLds q; pp::TLdsP p; };
+union TLdsAny { qp::TLds q; pp::TLdsP p; lp::TLdsL l; };
 
 // one workgroup of transcripts: `tl` lanes per proof (16: row form, 4: quad form); FORM 1: the
 // lane form, FORM 2: the pair form (kernels of their own, so that their register demand does
 // not touch the others')
 template <int FORM = 0>
-__device__ __forceinline__ void transcript_block(const DevCircuit& c, int tl, const TLdsAny& U) {
+__device__ __forceinline__ void transcript_block(const DevCircuit& c, int tl, TLdsAny& U) {
   const int g = blockIdx.x * 256 + threadIdx.x;
   const qp::TLds& T = U.q;
   if constexpr (FORM == 1) {
@@ -469,10 +483,18 @@ __device__ __forceinline__ void transcript_block(const DevCircuit& c, int tl, co
   } else if (tl == 16) {
     rp::Row R;
     rp::init(R, threadIdx.x);
-    if ((g >> 4) < c.B) transcript_row(c, g >> 4, R, T);
+    lp::Row LR;
+    lp::init(LR, U.l, threadIdx.x);
+    if ((g >> 4) < c.B) transcript_row(c, g >> 4, R, LR, T, U.l);
   } else {
     if ((g >> 2) < c.B) transcript_quad(c, g >> 2, g & 3, T);
   }
+}
+
+// the constant tables of the transcript form in use (tl uniform: 16 the row form, else quad)
+__device__ __forceinline__ void tlds_fill_form(TLdsAny& T, int tl) {
+  if (P2V_ROW_LAT && tl == 16) lp::tlds_fill(T.l, threadIdx.x, 256);
+  else qp::tlds_fill(T.q, threadIdx.x, 256);
 }
 
 // ------------------------------------------------------------------------ phase 1
@@ -485,7 +507,7 @@ __device__ __forceinline__ void phase1_body(const DevCircuit& c, int nt_blocks, 
   __shared__ TLdsAny T;
   if ((int)blockIdx.x < nt_blocks) {   // block-uniform branch: the whole workgroup fills T
     __builtin_amdgcn_s_setprio(3);
-    if constexpr (FORM == 0) qp::tlds_fill(T.q, threadIdx.x, 256);
+    if constexpr (FORM == 0) tlds_fill_form(T, tl);
     if constexpr (FORM == 2) pp::tlds_fill(T.p, threadIdx.x, 256);
     transcript_block<FORM>(c, tl, T);
     return;
@@ -513,7 +535,7 @@ extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_pe
 extern "C" __global__ void __launch_bounds__(256) k_transcript(DevCircuit c, int tl) {
   __builtin_amdgcn_s_setprio(3);
   __shared__ TLdsAny T;
-  qp::tlds_fill(T.q, threadIdx.x, 256);
+  tlds_fill_form(T, tl);
   transcript_block(c, tl, T);
 }
 // the lane and pair forms on their own (the lookahead / split launches, api.cpp)
@@ -534,7 +556,7 @@ extern "C" __global__ void __launch_bounds__(256) k_transcript_pair(DevCircuit c
 extern "C" __global__ void __launch_bounds__(256) k_transcript_x(DevCircuit c, int tl) {
   asm volatile("" ::: "v255", "a255");
   __shared__ TLdsAny T;
-  qp::tlds_fill(T.q, threadIdx.x, 256);
+  tlds_fill_form(T, tl);
   transcript_block(c, tl, T);
 }
 extern "C" __global__ void __launch_bounds__(256) k_leaf(DevCircuit c) {
@@ -606,16 +628,21 @@ __device__ __forceinline__ void merkle_unit(const DevCircuit& c) {
 extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCircuit c) { merkle_unit(c); }
 
 // Latency mode (small batches, api.cpp): the same paths in the row form of the permutation
-// (rposeidon.h: 16 lanes per path, lane L < 12 holding word L), four paths per wave.  A path is a
+// (lposeidon.h: 16 lanes per path, lane L < 12 holding word L), four paths per wave.  A path is a
 // chain of dependent compressions; one lane per path issues at the single-wave latency (~53 us
 // per compression, lat.hip), the row form at ~14 us.  Row = path (tree position, query, proof),
 // proofs fastest; lanes 0..3 hold the path value, lanes 4..7 the other half of the input.
 extern "C" __global__ void __launch_bounds__(256) k_merkle_row(DevCircuit c) {
-  __shared__ qp::TLds T;
-  qp::tlds_fill(T, threadIdx.x, 256);
+  __shared__ TLdsAny T;
+  tlds_fill_form(T, 16);
   __builtin_amdgcn_s_setprio(3);   // the batch's critical path in this mode
   rp::Row R;
   rp::init(R, threadIdx.x);
+  lp::Row LR;
+  lp::init(LR, T.l, threadIdx.x);
+  const qp::TLds& TQ = T.q;
+  const lp::TLdsL& TL = T.l;
+  (void)LR; (void)TQ; (void)TL;
   const int L = R.L;
   const int path = (int)((blockIdx.x * 256 + threadIdx.x) >> 4);
   const int npaths = c.Q * c.T * c.n;
@@ -640,7 +667,7 @@ extern "C" __global__ void __launch_bounds__(256) k_merkle_row(DevCircuit c) {
     const uint64_t cb = L == 4 ? c0 : L == 5 ? c1 : L == 6 ? c2 : c3;
     const bool odd = idx & 1u;
     const uint64_t x = L < 4 ? (odd ? sib : cur) : L < 8 ? (odd ? cb : sib) : 0;
-    cur = rp::permute(x, R, T);   // lanes 0..3: the compression's output
+    cur = ROW_PERMUTE(x);   // lanes 0..3: the compression's output
     idx >>= 1;
   }
   bool ok = idx < (uint32_t)c.cap_len;
@@ -932,13 +959,13 @@ extern "C" __global__ void __launch_bounds__(256) k_selftest(int op, const uint6
 }
 
 // The latency forms of the permutation on caller-chosen states (p2v_selftest ops 9-11; ADVICE
-// r4): 9 the row form (rposeidon.h, 16 lanes per state), 10 the quad form (qposeidon.h, 4 lanes),
+// r4): 9 the row form (lposeidon.h, or rposeidon.h with P2V_ROW_LAT=0; 16 lanes per state), 10 the quad form (qposeidon.h, 4 lanes),
 // 11 the pair form (pposeidon.h, 2 lanes).  Every lane of a group takes part in the DPP moves, so
 // lanes past n compute on a copy of state n - 1 and store nothing.  a, out: n states of 12 words.
 extern "C" __global__ void __launch_bounds__(256) k_selftest_forms(int op, const uint64_t* a, uint64_t* out, int64_t n) {
   __shared__ TLdsAny T;
   if (op == 11) pp::tlds_fill(T.p, threadIdx.x, 256);
-  else qp::tlds_fill(T.q, threadIdx.x, 256);
+  else tlds_fill_form(T, op == 9 ? 16 : 4);
   const int lanes = op == 9 ? 16 : op == 10 ? 4 : 2;
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t item = g / lanes, src = item < n ? item : n - 1;
@@ -948,7 +975,12 @@ extern "C" __global__ void __launch_bounds__(256) k_selftest_forms(int op, const
   if (op == 9) {
     rp::Row R;
     rp::init(R, threadIdx.x);
-    const uint64_t x = rp::permute(R.L < 12 ? s[R.L] : 0, R, T.q);
+    lp::Row LR;
+    lp::init(LR, T.l, threadIdx.x);
+    const qp::TLds& TQ = T.q;
+    const lp::TLdsL& TL = T.l;
+    (void)LR; (void)TQ; (void)TL;
+    const uint64_t x = ROW_PERMUTE(R.L < 12 ? s[R.L] : 0);
     if (item < n && R.L < 12) o[R.L] = x;
   } else if (op == 10) {
     uint64_t x[3] = {s[3 * t], s[3 * t + 1], s[3 * t + 2]};

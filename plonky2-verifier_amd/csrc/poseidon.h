@@ -296,14 +296,29 @@ namespace dv {
 // into 64-bit shifts of zero-extended register pairs).  The pair must lie inside the kernel's
 // SGPR budget: a build that forces a higher occupancy (e.g. amdgpu_waves_per_eu(7) on k_merkle)
 // makes hipcc warn "clobber list contains reserved registers: s94, s95", and is not valid.
+#ifndef P2V_MADK_C
+#define P2V_MADK_C 0   // 1: MDS MADs in plain C (measured slower, round 5: below)
+#endif
+// P2V_MADK_C = 1 writes the MDS MADs as plain C (a * C + acc, C an inline constant; powers of two
+// stay asm, the compiler would turn them into 64-bit shifts and masks), so that no s_nop pads them
+// as it pads every inline-asm statement with an SGPR output (k_merkle: 2 855 -> 2 219 static
+// s_nop).  Measured (profiles/r05c_madk.txt): the isolated permutation 3.22 -> 2.69 G perm/s
+// (generic) and 3.35 -> 2.71-2.80 (compression), the quick line 1.10 M: the compiler's schedule of
+// the plain MADs (more moves and 64-bit adds) costs far more than the padding.  Kept for the record.
 template <uint32_t C>
 __device__ __forceinline__ uint64_t madk(uint32_t a, uint64_t acc) {
+#if P2V_MADK_C
+  if constexpr ((C & (C - 1)) != 0) return (uint64_t)a * C + acc;
+#endif
   uint64_t d;
   asm("v_mad_u64_u32 %0, s[94:95], %1, %2, %3" : "=v"(d) : "v"(a), "n"(C), "v"(acc) : "s94", "s95");
   return d;
 }
 template <uint32_t C>
 __device__ __forceinline__ uint64_t madk_s(uint32_t a, uint64_t acc) {   // acc wave-uniform (SGPR pair)
+#if P2V_MADK_C
+  if constexpr ((C & (C - 1)) != 0) return (uint64_t)a * C + acc;
+#endif
   uint64_t d;
   asm("v_mad_u64_u32 %0, s[94:95], %1, %2, %3" : "=v"(d) : "v"(a), "n"(C), "s"(acc) : "s94", "s95");
   return d;

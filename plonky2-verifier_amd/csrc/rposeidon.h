@@ -102,6 +102,44 @@ __device__ __forceinline__ void conv(const Row& R, uint64_t v, uint64_t& al, uin
   ah = ah0 + ah1;
 }
 
+#ifndef P2V_ROW_SBOX
+#define P2V_ROW_SBOX 0
+#endif
+// The row form's S-box: a lone wave on its chain pays for every instruction it issues, so the
+// form matters here more than in the throughput kernels.  0: p2::sbox_lat_br (the S-box multiply
+// with one uniform branch per stage); 1: the multiply in plain C (the compiler's own carries:
+// no inline-asm statement, so no s_nop padding after one); 2: each multiply one asm block
+// (p2asm::mul_blk, 16 VALU, padding once per multiply); 3: p2::sbox_lat (branch-free).
+__device__ __forceinline__ uint64_t mul_c(uint64_t a, uint64_t b) {
+  const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+  const uint64_t p00 = (uint64_t)a0 * b0;
+  const uint64_t x = (uint64_t)a0 * b1 + (p00 >> 32);    // < 2^64
+  const uint64_t y = (uint64_t)a1 * b0 + x;              // may wrap: weight 2^96
+  const uint64_t cm = y < x ? 1 : 0;
+  const uint64_t hh = (uint64_t)a1 * b1 + (y >> 32);     // < 2^64
+  const uint64_t lo = (y << 32) | (uint32_t)p00;
+  // lo + h0 (2^32 - 1) - h1 - cm  (2^64 == 2^32 - 1, 2^96 == -1 mod p)
+  uint64_t t = (hh & 0xFFFFFFFFULL) * 0xFFFFFFFFULL + lo;
+  t += t < lo ? gl::EPS : 0;
+  const uint64_t d = (hh >> 32) + cm;                    // <= 2^32
+  uint64_t r = t - d;
+  r -= t < d ? gl::EPS : 0;
+  return r;
+}
+__device__ __forceinline__ uint64_t sbox_row(uint64_t x) {
+#if P2V_ROW_SBOX == 1
+  const uint64_t x2 = mul_c(x, x), x3 = mul_c(x, x2), x4 = mul_c(x2, x2);
+  return mul_c(x3, x4);
+#elif P2V_ROW_SBOX == 2 && defined(__HIP_DEVICE_COMPILE__)
+  const uint64_t x2 = p2asm::mul_blk(x, x), x3 = p2asm::mul_blk(x, x2), x4 = p2asm::mul_blk(x2, x2);
+  return p2asm::mul_blk(x3, x4);
+#elif P2V_ROW_SBOX == 3
+  return p2::sbox_lat(x);
+#else
+  return p2::sbox_lat_br(x);
+#endif
+}
+
 // this lane's round constant (idle lanes read word 11) as 32-bit halves, prefetched one
 // round ahead: it starts the lane's MDS accumulators of the previous round (the constant
 // addition folded into the MDS, as in p2::permute_dev)
@@ -123,10 +161,10 @@ __device__ __forceinline__ uint64_t permute(uint64_t x, const Row& R, const TT& 
     uint64_t al = nkl, ah = nkh;
     lane_rc(T.rc, r + 2 <= 30 ? r + 2 : 30, R.L, nkl, nkh);   // row 30 of the split table is zero
     if (r < 4 || r >= 26) {
-      conv(R, p2::sbox_lat_br(x), al, ah);
+      conv(R, sbox_row(x), al, ah);
     } else {
       conv(R, R.L == 0 ? 0 : x, al, ah);   // words 1..11: independent of the S-box chain
-      const uint64_t s = nbcast64<0>(p2::sbox_lat_br(x));
+      const uint64_t s = nbcast64<0>(sbox_row(x));
       al += (uint64_t)(uint32_t)s * R.col0;
       ah += (s >> 32) * R.col0;
     }

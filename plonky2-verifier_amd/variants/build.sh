@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 NAME=$1; EXTRA=$2
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -Werror=inline-asm $EXTRA"
 mkdir -p variants/build_$NAME
-for t in kernels vanish vanish_poseidon json_pack; do /opt/rocm/bin/hipcc $F -c -o variants/build_$NAME/$t.o csrc/$t.hip & done
+for t in kernels vanish vanish_poseidon json_pack util; do /opt/rocm/bin/hipcc $F -c -o variants/build_$NAME/$t.o csrc/$t.hip & done
 /opt/rocm/bin/hipcc $F -x hip -c -o variants/build_$NAME/api.o csrc/api.cpp &
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o variants/libp2v_$NAME.so variants/build_$NAME/*.o build/circuit.o

@@ -7,6 +7,7 @@
 #include "../../plonky2-verifier_amd/csrc/poseidon.h"
 #include "../../plonky2-verifier_amd/csrc/qposeidon.h"
 #include "../../plonky2-verifier_amd/csrc/rposeidon.h"
+#include "../../plonky2-verifier_amd/csrc/lposeidon.h"
 
 // ---- variant 1: lazy canonicalisation (values kept in [0, 2^64), canonical at the end)
 namespace v1 {
@@ -186,15 +187,31 @@ __global__ void __launch_bounds__(256) k_row_chain(uint64_t* st, int iters, int 
   if (L < 12) st[(size_t)L * nr + q] = x;
 }
 
+// the latency row form of lposeidon.h (round 5): same layout, LDS exchange + merged blocks
+__global__ void __launch_bounds__(256) k_lrow_chain(uint64_t* st, int iters, int nr) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = g >> 4, L = g & 15;
+  __shared__ lp::TLdsL T;
+  lp::tlds_fill(T, threadIdx.x, blockDim.x);
+  if (q >= nr) return;   // whole rows only (nr*16 threads)
+  lp::Row R;
+  lp::init(R, T, threadIdx.x);
+  uint64_t x = L < 12 ? st[(size_t)L * nr + q] : 0;
+  for (int it = 0; it < iters; it++) x = lp::permute(x, R, T);
+  if (L < 12) st[(size_t)L * nr + q] = x;
+}
+
 int main(int argc, char** argv) {
-  if (argc > 3 && atoi(argv[3]) == 8) {   // row chain latency: argv[1] = rows, argv[2] = chain length
+  if (argc > 3 && (atoi(argv[3]) == 8 || atoi(argv[3]) == 10)) {   // row chain latency: argv[1] = rows, argv[2] = chain length (10: lposeidon.h)
+    const bool lrow = atoi(argv[3]) == 10;
     int nr = atoi(argv[1]), iters = atoi(argv[2]);
     std::vector<uint64_t> h((size_t)12 * nr);
     for (size_t i = 0; i < h.size(); i++) h[i] = (i * 0x9E3779B97F4A7C15ULL) % gl::P;
     for (int i = 0; i < 12; i++) h[(size_t)i * nr] = i;
     uint64_t* d; CK(hipMalloc(&d, h.size() * 8));
     CK(hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice));
-    k_row_chain<<<(16 * nr + 255) / 256, 256>>>(d, 1, nr);
+    if (lrow) k_lrow_chain<<<(16 * nr + 255) / 256, 256>>>(d, 1, nr);
+    else k_row_chain<<<(16 * nr + 255) / 256, 256>>>(d, 1, nr);
     std::vector<uint64_t> o(h.size());
     CK(hipMemcpy(o.data(), d, o.size() * 8, hipMemcpyDeviceToHost));
     const uint64_t kat[12] = {0xd64e1e3efc5b8e9e, 0x53666633020aaa47, 0xd40285597c6a8825, 0x613a4f81e81231d2, 0x414754bfebd051f0, 0xcb1f8980294a023f,
@@ -206,13 +223,14 @@ int main(int argc, char** argv) {
       p2::permute(s);
       for (int i = 0; i < 12; i++) bad += s[i] != o[(size_t)i * nr + q];
     }
-    printf("row KAT %s, host mismatches %d\n", ok ? "ok" : "FAIL", bad);
+    printf("%s KAT %s, host mismatches %d\n", lrow ? "lrow" : "row", ok ? "ok" : "FAIL", bad);
     hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     CK(hipEventRecord(a));
-    k_row_chain<<<(16 * nr + 255) / 256, 256>>>(d, iters, nr);
+    if (lrow) k_lrow_chain<<<(16 * nr + 255) / 256, 256>>>(d, iters, nr);
+    else k_row_chain<<<(16 * nr + 255) / 256, 256>>>(d, iters, nr);
     CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
     float ms; CK(hipEventElapsedTime(&ms, a, b));
-    printf("row chain: %d rows x %d perms: %.3f ms, %.2f us per dependent permutation\n", nr, iters, ms, ms * 1e3 / iters);
+    printf("%s chain: %d rows x %d perms: %.3f ms, %.2f us per dependent permutation\n", lrow ? "lrow" : "row", nr, iters, ms, ms * 1e3 / iters);
     return ok && !bad ? 0 : 1;
   }
   if (argc > 3 && atoi(argv[3]) == 9) {   // quad chain latency: argv[1] = quads, argv[2] = chain length
