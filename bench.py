@@ -653,8 +653,8 @@ def main():
     ap.add_argument("--lookups", type=int, default=0,
                     help="0: standard recursion circuit (C2); 2: + LookupGate/LookupTableGate with a 256-entry and a 2^16-entry table (C3 circuit)")
     ap.add_argument("--transcript", choices=("auto", "row", "quad", "pair", "lane"), default="auto",
-                    help="transcript layout (P2V_TRANSCRIPT): auto = row below 2048 proofs per launch, quad from 2048, "
-                         "lane from 16384 (P2V_LANE_MIN)")
+                    help="transcript layout (P2V_TRANSCRIPT): auto = row below 4096 proofs per launch, quad from 4096 "
+                         "(P2V_QUAD_MIN), lane from 16384 (P2V_LANE_MIN)")
     ap.add_argument("--single-stream", action="store_true", help="P2V_SINGLE_STREAM=1: each workspace on one stream (no side stream)")
     ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES for this process (0: the runtime's default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -152,8 +152,13 @@ struct p2v_verifier {
   bool timed = false;
   bool fri_first = false;           // side stream order: k_fri before the vanishing kernels (env P2V_FRI_FIRST=1)
   int transcript_mode = 0;          // 0 auto, 1 row, 2 quad, 3 lane, 4 pair (env P2V_TRANSCRIPT)
-  int quad_min_batch = 2048;        // auto: quad form from this batch size on
+  int quad_min_batch = 4096;        // auto: quad form from this batch size on (env P2V_QUAD_MIN); round 5: with the
+                                    // latency row form (lposeidon.h) the row transcript wins up to 2048 proofs
+                                    // (2048: 2.40 against 2.98 ms serial, 1.084 against 1.077 M proofs/s at two in
+                                    // flight; 4096: the same serial, 1.13 against 1.225 M; profiles/r05h_*)
   int lane_min_batch = 16384;       // auto: lane form from this batch size on (env P2V_LANE_MIN)
+  int lat_max_batch = 64;           // latency mode (row-form Merkle paths, k_fri on its own stream) up to this
+                                    // batch size (env P2V_LAT_MAX, measurement)
   bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
   int side_prio = 0;                // env P2V_SIDE_PRIO=1: side stream at the device's highest priority (measured: no effect)
   int side_wg = 256;                // env P2V_SIDE_WG=64: one-wave groups for k_fri / k_vanish_final on the side stream
@@ -471,6 +476,8 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (const char* ff = getenv("P2V_FRI_FIRST")) v->fri_first = ff[0] == '1';
   if (const char* sw = getenv("P2V_SIDE_WG")) v->side_wg = atoi(sw) == 64 ? 64 : 256;
   if (const char* lm = getenv("P2V_LANE_MIN")) v->lane_min_batch = atoi(lm) > 0 ? atoi(lm) : v->lane_min_batch;
+  if (const char* qm = getenv("P2V_QUAD_MIN")) v->quad_min_batch = atoi(qm) > 0 ? atoi(qm) : v->quad_min_batch;
+  if (const char* lx = getenv("P2V_LAT_MAX")) v->lat_max_batch = atoi(lx) >= 0 ? atoi(lx) : v->lat_max_batch;
   if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : !strcmp(tm, "lane") ? 3 : !strcmp(tm, "pair") ? 4 : 0;
   DevCircuit& d = v->dc;
   memset(&d, 0, sizeof d);
@@ -722,7 +729,7 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   // phase 1: transcript waves + leaf-hash waves in one launch (the leaf sponges do not
   // depend on the challenges, so they fill the GPU while the serial transcripts run)
   // transcript form: the row form (16 lanes/proof) has the lowest latency, the quad form
-  // (4 lanes/proof) a lower total cost; batches from 2048 proofs hide the quad latency behind
+  // (4 lanes/proof) a lower total cost; batches from 4096 proofs hide the quad latency behind
   // their leaf hashing.  P2V_TRANSCRIPT=row|quad|lane|pair overrides (measurement).
   // From lane_min_batch on, the lane form (one lane per proof, about half of the quad's issue
   // cycles per proof: 85.9 M against 169.4 M VALU instructions per 4096 proofs, DESIGN.md §7.0,
@@ -818,7 +825,7 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   // path, 4x shorter chains, 16x the lanes), one-wave work-groups for k_fri, and k_fri on a stream
   // of its own beside the vanishing kernels instead of after them.  Measured:
   // one proof 2.19 -> 1.98 ms, 64 proofs 2.18 -> 2.10 ms; at 128 proofs the row form's lanes cost more than its latency saves
-  const bool lat = d.n <= 64;
+  const bool lat = d.n <= v->lat_max_batch;
   const int mk_wg = lat ? 64 : 256;
   const bool fri2 = lat && sd != st;
   if (fri2 && !v->side2) HCK(hipStreamCreateWithFlags(&v->side2, hipStreamNonBlocking));

@@ -140,7 +140,7 @@ __device__ __forceinline__ void chain_part(const uint64_t (&x)[6], const uint64_
 template <int D>
 __device__ __forceinline__ void pblock(uint64_t (&x)[6], int t, const p2::PBlock& B, const PBlockP& Q) {
   uint64_t y[D + 1];
-  y[1] = bcast64(p2::sbox_lat(x[0]), 0);   // word 0 lives in lane 0
+  y[1] = bcast64(qp::sbox_q(x[0]), 0);   // word 0 lives in lane 0
   uint64_t par[6];
 #pragma unroll
   for (int k = 0; k < 6; k++) par[k] = swap64(x[k]);
@@ -148,18 +148,18 @@ __device__ __forceinline__ void pblock(uint64_t (&x)[6], int t, const p2::PBlock
   uint64_t pl[D], ph[D];
   chain_part<1>(x, par, B, pl[1], ph[1]);
   if constexpr (D >= 3) chain_part<2>(x, par, B, pl[2], ph[2]);
-  y[2] = bcast64(p2::sbox_lat(p2::mds_reduce(pl[1], ph[1])), 0);
+  y[2] = bcast64(qp::sbox_q(p2::mds_reduce(pl[1], ph[1])), 0);
   if constexpr (D >= 4) chain_part<3>(x, par, B, pl[3], ph[3]);
   if constexpr (D >= 3) {
     constexpr uint32_t c = p2::mds_coeff(0, 0);
-    y[3] = bcast64(p2::sbox_lat(p2::mds_reduce(pl[2] + (uint64_t)(uint32_t)y[2] * c, ph[2] + (y[2] >> 32) * c)), 0);
+    y[3] = bcast64(qp::sbox_q(p2::mds_reduce(pl[2] + (uint64_t)(uint32_t)y[2] * c, ph[2] + (y[2] >> 32) * c)), 0);
   }
   if constexpr (D >= 4) {
     constexpr uint32_t c = p2::mds_coeff(0, 0);
     const uint32_t h2 = B.cf[1][12];
     const uint64_t al = pl[3] + (uint64_t)(uint32_t)y[2] * h2 + (uint64_t)(uint32_t)y[3] * c;
     const uint64_t ah = ph[3] + (y[2] >> 32) * h2 + (y[3] >> 32) * c;
-    y[4] = bcast64(p2::sbox_lat(p2::mds_reduce(al, ah)), 0);
+    y[4] = bcast64(qp::sbox_q(p2::mds_reduce(al, ah)), 0);
   }
   // output rows 6t + m: per-lane coefficients (LDS), one row at a time
   uint64_t out[6];
@@ -204,7 +204,7 @@ __device__ __forceinline__ void permute(uint64_t (&x)[6], int t, const TLdsP& T)
     }
     const int rr = r < 4 ? r : r + 22;   // 0..3, 26..29
 #pragma unroll
-    for (int k = 0; k < 6; k++) x[k] = p2::sbox_lat(x[k]);
+    for (int k = 0; k < 6; k++) x[k] = qp::sbox_q(x[k]);
     uint64_t par[6], out[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) par[k] = swap64(x[k]);

@@ -12,8 +12,23 @@
 #pragma once
 #include "gl.h"
 #include "poseidon.h"
+#include "lposeidon.h"
 
 namespace qp {
+
+#ifndef P2V_QUAD_SBOX
+#define P2V_QUAD_SBOX 1
+#endif
+// The chain's S-box (latency-bound waves: an instruction's cost is its issue slot, s_nop padding
+// included): 1 = the asm-block multiply of lposeidon.h (one statement, one padding per multiply,
+// round 5), 0 = p2::sbox_lat (the branch-free multiply, five asm statements per multiply)
+__device__ __forceinline__ uint64_t sbox_q(uint64_t x) {
+#if P2V_QUAD_SBOX && defined(__HIP_DEVICE_COMPILE__)
+  return lp::sbox(x);
+#else
+  return p2::sbox_lat(x);
+#endif
+}
 
 // quad_perm rotation: lane t reads lane (t + D) & 3
 template <int D>
@@ -169,7 +184,7 @@ template <int D>
 __device__ __forceinline__ void qblock(uint64_t x[3], int t, const p2::PBlock& B, const QBlock& Q) {
   // y1 = sbox(word 0) from lane 0; s' = the state with y1 in word 0
   uint64_t y[D + 1];
-  y[1] = bcast64(p2::sbox_lat(x[0]), 0);
+  y[1] = bcast64(sbox_q(x[0]), 0);
   x[0] = t == 0 ? y[1] : x[0];
   uint64_t X[4][3];
 #pragma unroll
@@ -181,11 +196,11 @@ __device__ __forceinline__ void qblock(uint64_t x[3], int t, const p2::PBlock& B
   chain_part<1>(X, B, pl[1], ph[1]);
   pl[1] = bcast64(pl[1], 0); ph[1] = bcast64(ph[1], 0);
   if constexpr (D >= 3) { chain_part<2>(X, B, pl[2], ph[2]); pl[2] = bcast64(pl[2], 0); ph[2] = bcast64(ph[2], 0); }
-  y[2] = p2::sbox_lat(p2::mds_reduce(pl[1], ph[1]));
+  y[2] = sbox_q(p2::mds_reduce(pl[1], ph[1]));
   if constexpr (D >= 4) { chain_part<3>(X, B, pl[3], ph[3]); pl[3] = bcast64(pl[3], 0); ph[3] = bcast64(ph[3], 0); }
   if constexpr (D >= 3) {
     constexpr uint32_t c = p2::mds_coeff(0, 0);
-    y[3] = p2::sbox_lat(p2::mds_reduce(pl[2] + (uint64_t)(uint32_t)y[2] * c, ph[2] + (y[2] >> 32) * c));
+    y[3] = sbox_q(p2::mds_reduce(pl[2] + (uint64_t)(uint32_t)y[2] * c, ph[2] + (y[2] >> 32) * c));
   }
   // per-lane output-row coefficients, one row at a time (row m + 1's loads overlap row m), the
   // first row's before the last S-box: 17 VGPRs in flight instead of 51
@@ -202,7 +217,7 @@ __device__ __forceinline__ void qblock(uint64_t x[3], int t, const p2::PBlock& B
     const uint64_t al = pl[3] + (uint64_t)(uint32_t)y[2] * h2 + (uint64_t)(uint32_t)y[3] * c;
     const uint64_t ah = ph[3] + (y[2] >> 32) * h2 + (y[3] >> 32) * c;
     load_row(0);
-    y[4] = p2::sbox_lat(p2::mds_reduce(al, ah));
+    y[4] = sbox_q(p2::mds_reduce(al, ah));
   } else {
     load_row(0);
   }
@@ -267,7 +282,7 @@ __device__ __forceinline__ void permute(uint64_t x[3], int t, const TLds& T) {
       x[0] = t == 0 ? 0 : w0;
       uint64_t al[3], ah[3];
       mds_acc(x, t, kl, kh, al, ah);
-      const uint64_t sb = bcast64(p2::sbox_lat(w0), 0);
+      const uint64_t sb = bcast64(sbox_q(w0), 0);
 #pragma unroll
       for (int m = 0; m < 3; m++) { al[m] += (uint64_t)(uint32_t)sb * col0[m]; ah[m] += (sb >> 32) * col0[m]; }
 #pragma unroll
@@ -280,7 +295,7 @@ __device__ __forceinline__ void permute(uint64_t x[3], int t, const TLds& T) {
     lane_rc(T.rc, rr + 2 <= 30 ? rr + 2 : 30, t, nkl, nkh);   // row 30 of the split table is zero
     uint64_t al[3], ah[3];
 #pragma unroll
-    for (int k = 0; k < 3; k++) x[k] = p2::sbox_lat(x[k]);
+    for (int k = 0; k < 3; k++) x[k] = sbox_q(x[k]);
     mds_acc(x, t, kl, kh, al, ah);
 #pragma unroll
     for (int m = 0; m < 3; m++) x[m] = p2::mds_reduce(al[m], ah[m]);
@@ -296,13 +311,13 @@ __device__ __forceinline__ void permute(uint64_t x[3], int t, const TLds& T) {
     uint64_t al[3], ah[3];
     if (r < 4 || r >= 26) {
 #pragma unroll
-      for (int k = 0; k < 3; k++) x[k] = p2::sbox_lat(x[k]);
+      for (int k = 0; k < 3; k++) x[k] = sbox_q(x[k]);
       mds_acc(x, t, kl, kh, al, ah);
     } else {
       const uint64_t w0 = x[0];
       x[0] = t == 0 ? 0 : w0;
       mds_acc(x, t, kl, kh, al, ah);           // independent of the S-box below
-      const uint64_t s = bcast64(p2::sbox_lat(w0), 0);
+      const uint64_t s = bcast64(sbox_q(w0), 0);
 #pragma unroll
       for (int m = 0; m < 3; m++) {
         al[m] += (uint64_t)(uint32_t)s * col0[m];
