@@ -769,10 +769,62 @@ __device__ E fold_generic(const DevCircuit& c, int s, int ab, int64_t off, int p
   return gl::escale(c.inv_arity[s], acc);
 }
 
+// ---- combineInitial's reduceWithPowers (Goldilocks.hs:180-183, Plonk/FRI.hs:151-207):
+// sum_v alpha^v y_v over a list of base-field leaf words (up to 5 contiguous segments of the
+// query's leaves, ascending), alpha in F^2.  Round 4 ran one F^2 Horner step per word (a full
+// emul, ~100 VALU).  Round 5: Horner in chunks of 8, g <- g alpha^8 + sum_{k<8} y_{j+k} alpha^k,
+// with alpha^1..alpha^8 in registers; the inner sum's base-field products y alpha^k (2 per word,
+// one per component) are accumulated unreduced in 128 + 3 bits and reduced once per chunk and
+// component.  The same field element (exact arithmetic).
+struct Acc3 { uint64_t lo, hi; uint32_t top; };   // lo + hi 2^64 + top 2^128
+__device__ __forceinline__ void acc_mul(Acc3& A, uint64_t y, uint64_t c) {
+  uint64_t h, l;
+  gl::mul128(y, c, h, l);
+  const uint64_t lo2 = A.lo + l;
+  const uint64_t c0 = lo2 < l ? 1 : 0;
+  const uint64_t hi2 = A.hi + h;
+  const uint32_t c1 = hi2 < h ? 1u : 0u;
+  const uint64_t hi3 = hi2 + c0;
+  const uint32_t c2 = hi3 < c0 ? 1u : 0u;
+  A.lo = lo2; A.hi = hi3; A.top += c1 + c2;
+}
+// lo + hi 2^64 + top 2^128 mod p, canonical: 2^128 == (2^32 - 1)^2 == -2^32 (mod p), top <= 8
+__device__ __forceinline__ uint64_t acc_reduce(const Acc3& A) {
+  return gl::sub(gl::reduce128(A.hi, A.lo), (uint64_t)A.top << 32);
+}
+struct Segs { int64_t off[5]; int n[5]; int ns; };
+__device__ __forceinline__ int64_t seg_addr(const Segs& S, int v) {   // v wave-uniform: scalar code
+  for (int s = 0; s < S.ns; s++) {
+    if (v < S.n[s]) return S.off[s] + v;
+    v -= S.n[s];
+  }
+  return S.off[0];
+}
+__device__ __forceinline__ E reduce_powers(const DevCircuit& c, const Segs& S, int p, E alpha, const E* ap) {
+  int N = 0;
+  for (int s = 0; s < S.ns; s++) N += S.n[s];
+  E g = gl::e0();
+  const int rem = N & 7;
+  for (int v = N - 1; v >= N - rem; v--) g = gl::eadd(gl::emul(g, alpha), gl::eb(ld(c, seg_addr(S, v), p)));
+  for (int j = N - rem - 8; j >= 0; j -= 8) {
+    uint64_t y[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) y[k] = ld(c, seg_addr(S, j + k), p);
+    Acc3 A{y[0], 0, 0}, B{0, 0, 0};   // alpha^0 = 1
+#pragma unroll
+    for (int k = 1; k < 8; k++) { acc_mul(A, y[k], ap[k].a); acc_mul(B, y[k], ap[k].b); }
+    g = gl::eadd(gl::emul(g, ap[8]), E{acc_reduce(A), acc_reduce(B)});
+  }
+  return g;
+}
+
 // k_fri runs on the side stream beside k_merkle (see vanish.hip P2V_SIDE_WAVES): 5 waves per SIMD
 // caps it at 96 VGPRs, so a wave fits where one k_merkle wave retired (0: compiler default, 122)
 #ifndef P2V_FOLD16_HALVES
 #define P2V_FOLD16_HALVES 1
+#endif
+#ifndef P2V_FRI_CHUNKED
+#define P2V_FRI_CHUNKED 1   // combineInitial in chunks of 8 with unreduced product sums (round 5, above)
 #endif
 #ifndef P2V_FRI_WAVES
 #define P2V_FRI_WAVES 5
@@ -799,6 +851,20 @@ extern "C" __global__ void __launch_bounds__(256) P2V_FRI_ATTR k_fri(DevCircuit 
   // quotient, lookup part; secondBatch = first r of the pp part, lookup part.
   const int npp_all = r * ((c.num_routed + c.qdf - 1) / c.qdf);
   const int64_t l0 = base + c.leaf[0], l1 = base + c.leaf[1], l2 = base + c.leaf[2], l3 = base + c.leaf[3];
+#if P2V_FRI_CHUNKED
+  // ascending lists (the Horner of round 4 below walks them from the top): firstBatch =
+  // leaf0 | leaf1 | leaf2[0, npp_all) | leaf3 | leaf2[npp_all, w2); secondBatch = leaf2[0, r') |
+  // leaf2[npp_all, w2)
+  E ap[9];
+  ap[0] = gl::eb(1); ap[1] = alpha;
+#pragma unroll
+  for (int k = 2; k <= 8; k++) ap[k] = gl::emul(ap[k - 1], alpha);
+  const int rr = r < npp_all ? r : npp_all;
+  Segs s0{{l0, l1, l2, l3, l2 + npp_all}, {c.width[0], c.width[1], npp_all, c.width[3], c.width[2] - npp_all}, 5};
+  Segs s1{{l2, l2 + npp_all, 0, 0, 0}, {rr, c.width[2] - npp_all, 0, 0, 0}, 2};
+  const E g0 = reduce_powers(c, s0, p, alpha, ap);
+  const E g1 = reduce_powers(c, s1, p, alpha, ap);
+#else
   E g0 = gl::e0(), g1 = gl::e0();
   for (int i = c.width[2] - 1; i >= npp_all; i--) g0 = gl::eadd(gl::emul(g0, alpha), gl::eb(ld(c, l2 + i, p)));
   for (int i = c.width[3] - 1; i >= 0; i--) g0 = gl::eadd(gl::emul(g0, alpha), gl::eb(ld(c, l3 + i, p)));
@@ -807,6 +873,7 @@ extern "C" __global__ void __launch_bounds__(256) P2V_FRI_ATTR k_fri(DevCircuit 
   for (int i = c.width[0] - 1; i >= 0; i--) g0 = gl::eadd(gl::emul(g0, alpha), gl::eb(ld(c, l0 + i, p)));
   for (int i = c.width[2] - 1; i >= npp_all; i--) g1 = gl::eadd(gl::emul(g1, alpha), gl::eb(ld(c, l2 + i, p)));
   for (int i = (r < npp_all ? r : npp_all) - 1; i >= 0; i--) g1 = gl::eadd(gl::emul(g1, alpha), gl::eb(ld(c, l2 + i, p)));
+#endif
   const int len2 = (r < npp_all ? r : npp_all) + (c.width[2] - npp_all);
   const uint64_t px = gl::mul(gl::MULT_GEN, pow_root(c, c.lde_bits, gl::rev_bits(c.lde_bits, idx)));
   const uint64_t omega = c.root_pow2[32 - c.degree_bits];

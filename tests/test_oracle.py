@@ -209,3 +209,56 @@ def test_first_round_wrap_states_hit_their_targets():
     assert exact > 0.6 * 12 * len(sbox_edge_values())   # y < min(rc0[i], 2^32 - 1): no 64-bit word reaches y itself
     st = first_round_wrap_states()
     assert any(add_nc(w, rc0[i]) == 1 << 48 for s in st for i, w in enumerate(s))
+
+
+def test_chunked_reduce_powers_algebra():
+    """k_fri's combineInitial (round 5, kernels.hip reduce_powers): Horner in chunks of 8,
+    g <- g a^8 + sum_{k<8} y_{j+k} a^k, whose inner sums of base-field products are kept as
+    lo + hi 2^64 + top 2^128 and reduced with 2^128 == -2^32 (mod p), equals the reference's
+    reduceWithPowers sum_i a^i y_i (Goldilocks.hs:180-183) in F^2 = F[X]/(X^2 - 7), for list
+    lengths that are and are not multiples of 8."""
+    import random
+    rng = random.Random(9)
+    assert pow(2, 128, P) == (P - (1 << 32)) % P
+
+    def emul(x, y):
+        return ((x[0] * y[0] + 7 * x[1] * y[1]) % P, (x[0] * y[1] + x[1] * y[0]) % P)
+
+    def acc_sum(ys, cs):   # the device accumulator: 64-bit words with explicit carries
+        lo = hi = top = 0
+        for y, c in zip(ys, cs):
+            prod = y * c
+            l, h = prod & ((1 << 64) - 1), prod >> 64
+            lo2 = (lo + l) & ((1 << 64) - 1)
+            c0 = 1 if lo2 < l else 0
+            hi2 = (hi + h) & ((1 << 64) - 1)
+            c1 = 1 if hi2 < h else 0
+            hi3 = (hi2 + c0) & ((1 << 64) - 1)
+            c2 = 1 if hi3 < c0 else 0
+            lo, hi, top = lo2, hi3, top + c1 + c2
+        assert top <= 8
+        r = (lo + hi * (1 << 64)) % P
+        return (r - (top << 32)) % P
+    for n in (1, 7, 8, 9, 16, 85, 135, 256, 258):
+        a = (rng.randrange(P), rng.randrange(P))
+        ys = [rng.randrange(P) for _ in range(n)]
+        ref = (0, 0)
+        pw = (1, 0)
+        for y in ys:
+            ref = ((ref[0] + pw[0] * y) % P, (ref[1] + pw[1] * y) % P)
+            pw = emul(pw, a)
+        ap = [(1, 0)]
+        for _ in range(8):
+            ap.append(emul(ap[-1], a))
+        g = (0, 0)
+        rem = n & 7
+        for v in range(n - 1, n - rem - 1, -1):
+            g = emul(g, a)
+            g = ((g[0] + ys[v]) % P, g[1])
+        for j in range(n - rem - 8, -1, -8):
+            ch = ys[j:j + 8]
+            sa = (ch[0] + acc_sum(ch[1:], [ap[k][0] for k in range(1, 8)])) % P
+            sb = acc_sum(ch[1:], [ap[k][1] for k in range(1, 8)])
+            g = emul(g, ap[8])
+            g = ((g[0] + sa) % P, (g[1] + sb) % P)
+        assert g == ref, n
