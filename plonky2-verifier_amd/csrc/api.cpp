@@ -31,6 +31,10 @@ extern "C" __global__ void k_transcript_x(DevCircuit, int);
 extern "C" __global__ void k_leaf(DevCircuit);
 extern "C" __global__ void k_merkle(DevCircuit);
 extern "C" __global__ void k_merkle_row(DevCircuit);
+extern "C" __global__ void k_merkle_plan(DevCircuit);
+extern "C" __global__ void k_merkle_cse(DevCircuit);
+extern "C" __global__ void k_merkle_fix(DevCircuit);
+extern "C" __global__ void k_merkle_resolve(DevCircuit);
 extern "C" __global__ void k_fri(DevCircuit);
 extern "C" __global__ void k_vanish_r2(DevCircuit);
 extern "C" __global__ void k_vanish_rn(DevCircuit);
@@ -129,6 +133,7 @@ struct p2v_verifier {
   DevCircuit dc{};
   std::vector<DevBuf> bufs;
   DevBuf in, soa, chal, leafdig, mk, fbits, qvals, van, vparts, lutre, lutpart, res, trace;
+  DevBuf m_plan, m_fol, m_chain, m_count, m_fix, m_badq, m_node;   // shared-node Merkle paths (dev.h mcse)
   DevBuf t_cs, t_kis, t_gkind, t_gpar, t_ggrp, t_gwoff, t_w, t_gs, t_ge, t_lin, t_lout, t_loff, t_llen, t_tw, t_ops, t_vit, t_rin, t_rout, t_roff, t_rch, t_pbase, t_pw;
   hipEvent_t ev[2 * kNumKernels];   // start/end per kernel
   hipEvent_t dep_p1 = nullptr, dep_side = nullptr, dep_tr = nullptr;
@@ -157,6 +162,7 @@ struct p2v_verifier {
                                     // (2048: 2.40 against 2.98 ms serial, 1.084 against 1.077 M proofs/s at two in
                                     // flight; 4096: the same serial, 1.13 against 1.225 M; profiles/r05h_*)
   int lane_min_batch = 16384;       // auto: lane form from this batch size on (env P2V_LANE_MIN)
+  bool merkle_cse = true;           // shared Merkle nodes hashed once (env P2V_MERKLE_CSE=0: one full path per lane)
   int lat_max_batch = 64;           // latency mode (row-form Merkle paths, k_fri on its own stream) up to this
                                     // batch size (env P2V_LAT_MAX, measurement)
   bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
@@ -425,7 +431,8 @@ void p2v_verifier_free(p2v_verifier* v) {
   (void)hipSetDevice(v->device);
   for (DevBuf* b : {&v->in, &v->soa, &v->chal, &v->leafdig, &v->mk, &v->fbits, &v->qvals, &v->van, &v->vparts, &v->lutre, &v->res, &v->trace, &v->t_cs, &v->t_kis,
                     &v->t_gkind, &v->t_gpar, &v->t_ggrp, &v->t_gwoff, &v->t_w, &v->t_gs, &v->t_ge, &v->t_lin, &v->t_lout, &v->t_loff, &v->t_llen, &v->t_tw, &v->t_ops, &v->t_vit, &v->t_rin, &v->t_rout, &v->t_roff, &v->t_rch, &v->t_pbase, &v->t_pw, &v->lutpart, &v->chal2, &v->j_blob, &v->j_offs, &v->j_skel, &v->j_tok, &v->j_ok,
-                    &v->b_rsrc, &v->b_rdst, &v->b_rlen, &v->b_coff, &v->b_cval})
+                    &v->b_rsrc, &v->b_rdst, &v->b_rlen, &v->b_coff, &v->b_cval,
+                    &v->m_plan, &v->m_fol, &v->m_chain, &v->m_count, &v->m_fix, &v->m_badq, &v->m_node})
     b->free_();
   if (v->timed) for (auto& e : v->ev) (void)hipEventDestroy(e);
   if (v->dep_p1) (void)hipEventDestroy(v->dep_p1);
@@ -477,6 +484,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (const char* sw = getenv("P2V_SIDE_WG")) v->side_wg = atoi(sw) == 64 ? 64 : 256;
   if (const char* lm = getenv("P2V_LANE_MIN")) v->lane_min_batch = atoi(lm) > 0 ? atoi(lm) : v->lane_min_batch;
   if (const char* qm = getenv("P2V_QUAD_MIN")) v->quad_min_batch = atoi(qm) > 0 ? atoi(qm) : v->quad_min_batch;
+  if (const char* mc = getenv("P2V_MERKLE_CSE")) v->merkle_cse = mc[0] != '0';
   if (const char* lx = getenv("P2V_LAT_MAX")) v->lat_max_batch = atoi(lx) >= 0 ? atoi(lx) : v->lat_max_batch;
   if (const char* tm = getenv("P2V_TRANSCRIPT")) v->transcript_mode = !strcmp(tm, "row") ? 1 : !strcmp(tm, "quad") ? 2 : !strcmp(tm, "lane") ? 3 : !strcmp(tm, "pair") ? 4 : 0;
   DevCircuit& d = v->dc;
@@ -630,6 +638,24 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
   if (e == hipSuccess) e = v->res.alloc(B);
   if (e == hipSuccess) e = hipHostMalloc((void**)&v->h_res, B);
   if (e == hipSuccess) e = v->trace.alloc((size_t)C.trace_words * B * 8);
+  // shared-node Merkle paths: on unless P2V_MERKLE_CSE=0 or the shape exceeds the plan's fields
+  d.mcse = v->merkle_cse && d.Q <= P2V_CSE_MAX_Q && d.depth0 <= P2V_CSE_MAX_DEPTH && B <= (size_t)P2V_CSE_MAX_B && d.T < 32;
+  if (d.mcse) {
+    const size_t ncls = 1 + (size_t)d.S, nb = 1 + (size_t)d.depth0;
+    d.mcap = (int64_t)d.T * d.Q * (int64_t)B;
+    if (e == hipSuccess) e = v->m_plan.alloc(ncls * d.Q * B * 4);
+    if (e == hipSuccess) e = v->m_fol.alloc(ncls * d.Q * B * 8);
+    if (e == hipSuccess) e = v->m_chain.alloc(nb * (size_t)d.mcap * 4);
+    const size_t cnt_bytes = (nb + 1) * 64;   // bucket counters and the fix-list length, 64 B apart
+    if (e == hipSuccess) e = v->m_count.alloc(cnt_bytes);
+    if (e == hipSuccess) e = hipMemset(v->m_count.p, 0, cnt_bytes);   // then zeroed by each run's k_merkle_resolve
+    if (e == hipSuccess) e = v->m_fix.alloc((size_t)d.mcap * 4);
+    if (e == hipSuccess) e = v->m_badq.alloc((size_t)d.T * d.Q * B);
+    if (e == hipSuccess) e = v->m_node.alloc((size_t)d.T * d.Q * 4 * B * 8);
+    d.mplan = (uint32_t*)v->m_plan.p; d.mfol = (uint64_t*)v->m_fol.p; d.mchain = (uint32_t*)v->m_chain.p;
+    d.mcount = (int32_t*)v->m_count.p; d.mfixn = d.mcount + nb * 16; d.mfix = (uint32_t*)v->m_fix.p;
+    d.mbadq = (uint8_t*)v->m_badq.p; d.mnode = (uint64_t*)v->m_node.p;
+  }
   if (e == hipSuccess) { for (auto& x : v->ev) { e = hipEventCreate(&x); if (e != hipSuccess) break; } v->timed = e == hipSuccess; }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_p1, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&v->dep_side, hipEventDisableTiming);
@@ -902,7 +928,20 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   T0(2, st);
   const int merkle_units = d.Q * d.T * NPB;
   if (lat) k_merkle_row<<<(unsigned)(((int64_t)d.Q * d.T * d.n * 16 + 255) / 256), 256, 0, st>>>(d);
-  else k_merkle<<<(merkle_units + 3) / 4, 256, 0, st>>>(d);
+  else if (d.mcse) {
+    // shared nodes once: plan + bucketed chains + followers' statuses (kernels.hip); the chain
+    // grid covers every bucket's last partial wave
+    const int ncls = 1 + d.S;
+    k_merkle_plan<<<(ncls * d.Q * NPB + 15) / 16, 1024, 0, st>>>(d);
+    DBG("k_merkle_plan", st);
+    const int64_t cse_waves = ((int64_t)d.T * d.Q * d.n + 63) / 64 + d.depth0 + 1;
+    k_merkle_cse<<<(unsigned)((cse_waves + 3) / 4), 256, 0, st>>>(d);
+    DBG("k_merkle_cse", st);
+    k_merkle_fix<<<256, 256, 0, st>>>(d);   // grid-stride over the (usually empty) list
+    DBG("k_merkle_fix", st);
+    k_merkle_resolve<<<(merkle_units + 3) / 4, 256, 0, st>>>(d);
+    DBG("k_merkle_resolve", st);
+  } else k_merkle<<<(merkle_units + 3) / 4, 256, 0, st>>>(d);
   DBG("k_merkle", st);
   T1(2, st);
   if (sd != st) HCK(hipStreamWaitEvent(st, v->dep_side, 0));

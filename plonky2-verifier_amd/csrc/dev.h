@@ -81,7 +81,22 @@ struct DevCircuit {
   uint64_t* vparts;                // [n_vitems][2r][B]: per-item partial alpha-sums
   uint64_t* lutre;                 // [r][nluts][B]: evalFinalRE values (debug trace)
   uint64_t* lutpart;               // [r][n_lut_pieces][B]: k_lut partial sums
+  // Merkle paths with every shared node hashed once (kernels.hip k_merkle_plan / k_merkle_cse /
+  // k_merkle_fix / k_merkle_resolve; mcse = 0: k_merkle, one full path per lane)
+  int32_t mcse;
+  int64_t mcap;                    // chains per bucket (T * Q * Bmax)
+  uint32_t* mplan;                 // [1 + S][Q][B]: e | owner << 4 | same_leaf << 9 | root << 10
+  uint64_t* mfol;                  // [1 + S][Q][B]: per owned level l, bits 5l..5l+4: the follower (31: none)
+  uint32_t* mchain;                // [depth0 + 1][mcap]: chain ids t << 27 | q << 22 | p, bucket = chain length
+  int32_t* mcount;                 // [depth0 + 1] x 16: chains per bucket, 64 B apart (k_merkle_resolve zeroes them)
+  int32_t* mfixn;                  // flagged followers listed in mfix (k_merkle_resolve zeroes it)
+  uint32_t* mfix;                  // [mcap]: chain ids of the followers k_merkle_fix re-runs
+  uint8_t* mbadq;                  // [T][Q][B]: the follower failed a shared-node check
+  uint64_t* mnode;                 // [T][Q][4][B]: a follower's node at its meeting level
 };
+#define P2V_CSE_MAX_DEPTH 12       // 5-bit follower fields of one u64 per owned level
+#define P2V_CSE_MAX_Q 31           // 5-bit query ids, 31 = none
+#define P2V_CSE_MAX_B (1 << 22)    // 22-bit proof index in a chain id
 
 // transcript op program (built on the host from the circuit; uniform across the batch)
 #define TOP_ABSORB_SOA 0    // absorb n words of the proof (SoA) from word a

@@ -573,17 +573,11 @@ extern "C" __global__ void __launch_bounds__(256) k_leaf(DevCircuit c) {
 #else
 #define P2V_MERKLE_ATTR
 #endif
-__device__ __forceinline__ void merkle_unit(const DevCircuit& c) {
-  const int lane = threadIdx.x & 63;
-  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int NPB = c.B >> 6;
-  if (unit >= c.Q * c.T * NPB) return;
-  const int pb = unit % NPB, qt = unit / NPB;   // (position, query)-major: deepest paths first
-  const int q = qt % c.Q, t = c.merkle_order[qt / c.Q];
-  const int p = pb * 64 + lane;
+// Tree t of query q (lane proof p): path length, word offset of its siblings in the proof, and the
+// query's leaf index in that tree (FRI step trees: the index shifted by the earlier arities)
+__device__ __forceinline__ void tree_path(const DevCircuit& c, int t, int q, int p, int& depth, int64_t& poff, uint32_t& idx) {
   const int64_t base = c.q0 + (int64_t)q * c.qstride;
-  uint32_t idx = (uint32_t)chal(c, CH_QIDX(c) + q, p);
-  int depth; int64_t poff;
+  idx = (uint32_t)chal(c, CH_QIDX(c) + q, p);
   if (t < 4) { depth = c.depth0; poff = base + c.path[t]; }
   else {
     const int s = t - 4;
@@ -591,26 +585,23 @@ __device__ __forceinline__ void merkle_unit(const DevCircuit& c) {
     for (int j = 0; j <= s; j++) sh += c.arity[j];
     idx >>= sh; depth = c.step_depth[s]; poff = base + c.step_path[s];
   }
-  uint64_t* src = c.leafdig + ((int64_t)(q * c.T + t) * 4) * c.B + p;
-  uint64_t cur[4];
+}
+__device__ __forceinline__ void load_leafdig(const DevCircuit& c, int t, int q, int p, uint64_t (&cur)[4]) {
+  const uint64_t* src = c.leafdig + ((int64_t)(q * c.T + t) * 4) * c.B + p;
 #pragma unroll
   for (int i = 0; i < 4; i++) cur[i] = src[(int64_t)i * c.B];
-  for (int l = 0; l < depth; l++) {   // even index: compress(cur, sib), odd: compress(sib, cur)
-    uint64_t sib[4];
-    // one level's 32 B of siblings per load (proof-major: the line re-fetches this leaves hit
-    // the Infinity Cache; tiled: whole 512-B rows per wave)
+}
+// One level of a path (Hash/Merkle.hs:27-42): even index compress(cur, sib), odd compress(sib, cur)
+__device__ __forceinline__ void merkle_level(uint64_t (&cur)[4], const uint64_t (&sib)[4], bool odd) {
+  uint64_t st[12];
 #pragma unroll
-    for (int i = 0; i < 4; i++) sib[i] = ld(c, poff + 4 * l + i, p);
-    const bool odd = idx & 1u;
-    uint64_t st[12];
+  for (int i = 0; i < 4; i++) { st[i] = odd ? sib[i] : cur[i]; st[4 + i] = odd ? cur[i] : sib[i]; st[8 + i] = 0; }
+  p2::permute_dev(st, true, 1);   // compress: words 8..11 enter as 0, only 0..3 are read
 #pragma unroll
-    for (int i = 0; i < 4; i++) { st[i] = odd ? sib[i] : cur[i]; st[4 + i] = odd ? cur[i] : sib[i]; st[8 + i] = 0; }
-    p2::permute_dev(st, true, 1);   // compress: words 8..11 enter as 0, only 0..3 are read
-#pragma unroll
-    for (int i = 0; i < 4; i++) cur[i] = st[i];
-    idx >>= 1;
-  }
-  // cap_roots !! (idx >> depth)
+  for (int i = 0; i < 4; i++) cur[i] = st[i];
+}
+// cap_roots !! (idx >> depth) == the path's root
+__device__ __forceinline__ bool cap_ok(const DevCircuit& c, int t, uint32_t idx, const uint64_t (&cur)[4], int p) {
   bool ok = idx < (uint32_t)c.cap_len;
   const uint32_t ci = ok ? idx : 0;
 #pragma unroll
@@ -623,9 +614,280 @@ __device__ __forceinline__ void merkle_unit(const DevCircuit& c) {
     else root = ld(c, c.ccaps + (int64_t)(t - 4) * 4 * c.cap_len + ci * 4 + i, p);
     ok = ok && (root == cur[i]);
   }
-  c.mk_ok[(int64_t)(q * c.T + t) * c.B + p] = ok ? 1 : 0;
+  return ok;
+}
+// The whole path of (tree t, query q, proof p) against its cap entry
+__device__ __forceinline__ bool path_ok(const DevCircuit& c, int t, int q, int p) {
+  int depth; int64_t poff; uint32_t idx;
+  tree_path(c, t, q, p, depth, poff, idx);
+  uint64_t cur[4];
+  load_leafdig(c, t, q, p, cur);
+  for (int l = 0; l < depth; l++) {
+    uint64_t sib[4];
+    // one level's 32 B of siblings per load (proof-major: the line re-fetches this leaves hit
+    // the Infinity Cache; tiled: whole 512-B rows per wave)
+#pragma unroll
+    for (int i = 0; i < 4; i++) sib[i] = ld(c, poff + 4 * l + i, p);
+    merkle_level(cur, sib, idx & 1u);
+    idx >>= 1;
+  }
+  return cap_ok(c, t, idx, cur, p);
+}
+__device__ __forceinline__ void merkle_unit(const DevCircuit& c) {
+  const int lane = threadIdx.x & 63;
+  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int NPB = c.B >> 6;
+  if (unit >= c.Q * c.T * NPB) return;
+  const int pb = unit % NPB, qt = unit / NPB;   // (position, query)-major: deepest paths first
+  const int q = qt % c.Q, t = c.merkle_order[qt / c.Q];
+  const int p = pb * 64 + lane;
+  c.mk_ok[(int64_t)(q * c.T + t) * c.B + p] = path_ok(c, t, q, p) ? 1 : 0;
 }
 extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCircuit c) { merkle_unit(c); }
+
+// ------------------------------------------------------------------------ Merkle paths, shared nodes once
+// The Q queries of a proof open paths in the same trees, and two queries whose leaf indices agree
+// above bit l hash the same parent at level l and everything above it: with 28 queries and cap 16
+// a third of the top-level compressions repeat (13.4 % of all compressions of the standard proof).
+// Each parent is hashed once, by its OWNER, the lowest query under it.  Query q owns the levels
+// 0 .. e_q - 1 (a prefix: ownership only shrinks going up), so its work is one chain of e_q
+// compressions; at level e_q < depth it meets its owner o (a lower query) and stops.
+// Exact, whatever the proof holds.  q's reference path equals o's above level e_q when both
+// compress the same pair there and read the same siblings above it, so for every follower q
+//   (A) o's sibling at level e_q is q's node (same leaf, e_q = 0: the leaf digests are equal),
+//   (B) q's sibling at level e_q is o's node (checked by o's chain, which knows its follower there),
+//   (C) q's and o's siblings above level e_q are equal (same leaf: from level 0 on),
+// and then q's status is o's.  A follower that fails a check is flagged and re-run from its own
+// node at level e_q (k_merkle_fix), unless its root (the lowest query under its cap entry, whose
+// chain is a whole path) failed: then k_status stops at that lower query whatever q's status is
+// (Plonk/FRI.hs:105-117, queries in order).  Statuses and codes are the plain k_merkle's bit for
+// bit; honest proofs fail no check.
+//   k_merkle_plan     one lane per (tree class, query, proof): e, owner, followers, root; appends
+//                     the chains to buckets by length, one global atomic per (work-group, bucket)
+//                     (the 4 initial trees share the leaf index, each FRI step tree shifts it)
+//   k_merkle_cse      one lane per chain, longest bucket first: waves of equal-length chains
+//   k_merkle_fix      the flagged followers (a compact list; none for honest proofs)
+//   k_merkle_resolve  one lane per (tree, query, proof): a follower takes the status of its
+//                     first flagged or root ancestor
+#define P2V_CSE_CSTRIDE 16   // counters 64 B apart: atomics on one line serialise
+__device__ __forceinline__ void class_shape(const DevCircuit& c, int cls, int& sh, int& depth) {
+  sh = 0; depth = c.depth0;
+  if (cls > 0) { for (int j = 0; j < cls; j++) sh += c.arity[j]; depth = c.step_depth[cls - 1]; }
+}
+__device__ __forceinline__ int tree_class(int t) { return t < 4 ? 0 : t - 3; }
+extern "C" __global__ void __launch_bounds__(1024) k_merkle_plan(DevCircuit c) {
+  __shared__ int hist[P2V_CSE_MAX_DEPTH + 1], gbase[P2V_CSE_MAX_DEPTH + 1];
+  const int lane = threadIdx.x & 63;
+  const int unit = blockIdx.x * 16 + (threadIdx.x >> 6);
+  const int NPB = c.B >> 6, ncls = 1 + c.S;
+  const int nb = c.depth0 + 1;
+  if (threadIdx.x < (unsigned)nb) hist[threadIdx.x] = 0;
+  __syncthreads();
+  const bool unit_live = unit < ncls * c.Q * NPB;   // wave-uniform
+  const int pb = unit % NPB, cq = unit / NPB;
+  const int q = cq % c.Q, cls = unit_live ? cq / c.Q : 0;
+  const int p = pb * 64 + lane;
+  const bool live = unit_live && p < c.n;
+  int sh, depth;
+  class_shape(c, cls, sh, depth);
+  const int ntr = cls == 0 ? 4 : 1, t0 = cls == 0 ? 0 : 3 + cls;
+  int e = 0, loc = 0, cnt = 0;
+  if (live) {
+    const uint64_t* qi = c.chal + (int64_t)CH_QIDX(c) * c.B + p;
+    const uint32_t me = (uint32_t)qi[(int64_t)q * c.B] >> sh;
+    // b = bit length of (index xor other's index): the two paths first share a parent at level b - 1
+    int minb = 64, owner = q, root = q;
+    bool have_root = false;
+    uint64_t fol = ~0ULL;
+    for (int k0 = 0; k0 < c.Q; k0 += 4) {
+      uint32_t ik[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) ik[u] = k0 + u < c.Q ? (uint32_t)qi[(int64_t)(k0 + u) * c.B] >> sh : me;
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int k = k0 + u;
+        if (k >= c.Q) break;
+        const uint32_t x = me ^ ik[u];
+        const int b = x ? 32 - __clz(x) : 0;
+        if (!have_root && b <= depth) { root = k; have_root = true; }   // lowest query under the cap entry
+        if (k < q) {
+          if (b < minb) { minb = b; owner = k; }   // the lowest query sharing q's lowest shared parent
+        } else if (k > q && b >= 1 && b <= depth) {
+          // the lowest query in the sibling subtree at level b - 1 meets q there (if q owns that level)
+          const int sl = 5 * (b - 1);
+          if (((fol >> sl) & 31) == 31) fol ^= (uint64_t)(31 ^ k) << sl;
+        }
+      }
+    }
+    e = minb - 1 >= depth ? depth : (minb >= 1 ? minb - 1 : 0);
+    if (e < depth) fol |= ~0ULL << (5 * e);   // levels q does not own: their owner checks the follower
+    const int64_t pi = ((int64_t)cls * c.Q + q) * c.B + p;
+    c.mplan[pi] = (uint32_t)e | (uint32_t)owner << 4 | (uint32_t)(minb == 0) << 9 | (uint32_t)root << 10;
+    c.mfol[pi] = fol;
+    for (int tt = 0; tt < ntr; tt++) c.mbadq[((int64_t)(t0 + tt) * c.Q + q) * c.B + p] = 0;
+  }
+  // the wave's lanes of one length: one run of that bucket, tree-major; a work-group's runs are
+  // packed in LDS, then one global atomic per (work-group, bucket) places them
+  uint64_t todo = __ballot(live);
+  while (todo) {
+    const int lead = __ffsll((unsigned long long)todo) - 1;
+    const int eb = __shfl(e, lead);
+    const uint64_t grp = __ballot(live && e == eb);
+    const int n = __popcll(grp);
+    int off = 0;
+    if (lane == lead) off = atomicAdd(&hist[eb], n * ntr);
+    off = __shfl(off, lead);
+    if (live && e == eb) { loc = off + __popcll(grp & ((1ULL << lane) - 1)); cnt = n; }
+    todo &= ~grp;
+  }
+  __syncthreads();
+  if (threadIdx.x < (unsigned)nb) {
+    const int h = hist[threadIdx.x];
+    gbase[threadIdx.x] = h ? atomicAdd(&c.mcount[threadIdx.x * P2V_CSE_CSTRIDE], h) : 0;
+  }
+  __syncthreads();
+  if (live) {
+    uint32_t* dst = c.mchain + (int64_t)e * c.mcap;
+    const int64_t base = (int64_t)gbase[e] + loc;
+    for (int tt = 0; tt < ntr; tt++) {
+      const int64_t pos = base + (int64_t)tt * cnt;
+      if (pos < c.mcap) dst[pos] = (uint32_t)(t0 + tt) << 27 | (uint32_t)q << 22 | (uint32_t)p;   // (always: T Q B slots)
+    }
+  }
+}
+// a follower to re-run from its own node (k_merkle_fix): flag + list entry
+__device__ __forceinline__ void cse_flag(const DevCircuit& c, int t, int q, int p) {
+  c.mbadq[((int64_t)t * c.Q + q) * c.B + p] = 1;
+  const int at = atomicAdd(c.mfixn, 1);
+  if (at < c.mcap) c.mfix[at] = (uint32_t)t << 27 | (uint32_t)q << 22 | (uint32_t)p;
+}
+__device__ __forceinline__ void merkle_chain(const DevCircuit& c) {
+  const int lane = threadIdx.x & 63;
+  int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  int b = c.depth0;   // longest chains first
+  int cnt = 0;
+  for (; b >= 0; b--) {
+    cnt = (int)min((int64_t)c.mcount[b * P2V_CSE_CSTRIDE], c.mcap);
+    const int nw = (cnt + 63) >> 6;
+    if (w < nw) break;
+    w -= nw;
+  }
+  if (b < 0) return;
+  const int slot = w * 64 + lane;
+  if (slot >= cnt) return;
+  const uint32_t id = c.mchain[(int64_t)b * c.mcap + slot];
+  const int t = (int)(id >> 27), q = (int)((id >> 22) & 31), p = (int)(id & 0x3FFFFFu);
+  const int64_t pi = ((int64_t)tree_class(t) * c.Q + q) * c.B + p;
+  const uint32_t pw = c.mplan[pi];
+  const uint64_t fol = c.mfol[pi];
+  const int e = b;   // == pw & 15: the bucket is the chain length (wave-uniform)
+  int depth; int64_t poff; uint32_t idx;
+  tree_path(c, t, q, p, depth, poff, idx);
+  uint64_t cur[4];
+  load_leafdig(c, t, q, p, cur);
+  for (int l = 0; l < e; l++) {
+    uint64_t sib[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) sib[i] = ld(c, poff + 4 * l + i, p);
+    const int f = (int)((fol >> (5 * l)) & 31);
+    if (f != 31) {   // (B): the follower meeting this path here holds this node as its sibling
+      const int64_t fo = poff + (int64_t)(f - q) * c.qstride + 4 * l;
+      bool bad = false;
+#pragma unroll
+      for (int i = 0; i < 4; i++) bad |= ld(c, fo + i, p) != cur[i];
+      if (bad) cse_flag(c, t, f, p);
+    }
+    merkle_level(cur, sib, idx & 1u);
+    idx >>= 1;
+  }
+  if (e == depth) {
+    c.mk_ok[(int64_t)(q * c.T + t) * c.B + p] = cap_ok(c, t, idx, cur, p) ? 1 : 0;
+    return;
+  }
+  uint64_t* nd = c.mnode + ((int64_t)(t * c.Q + q) * 4) * c.B + p;   // k_merkle_fix resumes here
+#pragma unroll
+  for (int i = 0; i < 4; i++) nd[(int64_t)i * c.B] = cur[i];
+  const int owner = (int)((pw >> 4) & 31);
+  const int64_t oo = poff + (int64_t)(owner - q) * c.qstride;   // the owner's siblings in this tree
+  bool bad = false;
+  int l0 = e + 1;
+  if ((pw >> 9) & 1) {   // same leaf: equal digests, and (C) from level 0
+    uint64_t od[4];
+    load_leafdig(c, t, owner, p, od);
+#pragma unroll
+    for (int i = 0; i < 4; i++) bad |= od[i] != cur[i];
+    l0 = 0;
+  } else {   // (A)
+#pragma unroll
+    for (int i = 0; i < 4; i++) bad |= ld(c, oo + 4 * e + i, p) != cur[i];
+  }
+  for (int l = l0; l < depth; l++)   // (C)
+#pragma unroll
+    for (int i = 0; i < 4; i++) bad |= ld(c, poff + 4 * l + i, p) != ld(c, oo + 4 * l + i, p);
+  if (bad) cse_flag(c, t, q, p);
+}
+#ifndef P2V_CSE_WAVES
+#define P2V_CSE_WAVES 6   // amdgpu_waves_per_eu on k_merkle_cse (80 VGPRs; the spills sit outside the chain loop)
+#endif
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P2V_CSE_WAVES))) k_merkle_cse(DevCircuit c) { merkle_chain(c); }
+// The flagged followers, each from its own node at its meeting level to its cap entry (grid-stride
+// over the list; the list length is read once)
+extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle_fix(DevCircuit c) {
+  const int64_t nfix = min((int64_t)*c.mfixn, c.mcap);
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nfix; k += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t id = c.mfix[k];
+    const int t = (int)(id >> 27), q = (int)((id >> 22) & 31), p = (int)(id & 0x3FFFFFu);
+    const uint32_t pw = c.mplan[((int64_t)tree_class(t) * c.Q + q) * c.B + p];
+    uint8_t* mk = c.mk_ok + (int64_t)t * c.B + p;
+    const int64_t qs = (int64_t)c.T * c.B;
+    if (!mk[(int64_t)((pw >> 10) & 31) * qs]) { mk[q * qs] = 0; continue; }   // a lower query fails first
+    const int e = (int)(pw & 15);
+    int depth; int64_t poff; uint32_t idx;
+    tree_path(c, t, q, p, depth, poff, idx);
+    uint64_t cur[4];
+    const uint64_t* nd = c.mnode + ((int64_t)(t * c.Q + q) * 4) * c.B + p;
+#pragma unroll
+    for (int i = 0; i < 4; i++) cur[i] = nd[(int64_t)i * c.B];
+    idx >>= e;
+    for (int l = e; l < depth; l++) {
+      uint64_t sib[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) sib[i] = ld(c, poff + 4 * l + i, p);
+      merkle_level(cur, sib, idx & 1u);
+      idx >>= 1;
+    }
+    mk[q * qs] = cap_ok(c, t, idx, cur, p) ? 1 : 0;
+  }
+}
+extern "C" __global__ void __launch_bounds__(256) k_merkle_resolve(DevCircuit c) {
+  if (blockIdx.x == 0 && threadIdx.x <= (unsigned)c.depth0) c.mcount[threadIdx.x * P2V_CSE_CSTRIDE] = 0;   // the next run's
+  if (blockIdx.x == 0 && threadIdx.x == 0) *c.mfixn = 0;
+  const int lane = threadIdx.x & 63;
+  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int NPB = c.B >> 6;
+  if (unit >= c.Q * c.T * NPB) return;
+  const int pb = unit % NPB, qt = unit / NPB;
+  const int q = qt % c.Q, t = qt / c.Q;
+  const int p = pb * 64 + lane;
+  if (p >= c.n) return;
+  const int cls = tree_class(t);
+  int sh, depth;
+  class_shape(c, cls, sh, depth);
+  const uint32_t* plan = c.mplan + (int64_t)cls * c.Q * c.B + p;
+  const uint8_t* badq = c.mbadq + (int64_t)t * c.Q * c.B + p;
+  uint32_t pw = plan[(int64_t)q * c.B];
+  if ((int)(pw & 15) == depth || badq[(int64_t)q * c.B]) return;   // a root or a re-run follower: written
+  // the first ancestor whose status is its own: a root chain or a re-run follower
+  int a = (int)((pw >> 4) & 31);
+  for (int hop = 0; hop < c.Q; hop++) {
+    pw = plan[(int64_t)a * c.B];
+    if ((int)(pw & 15) == depth || badq[(int64_t)a * c.B]) break;
+    a = (int)((pw >> 4) & 31);
+  }
+  uint8_t* mk = c.mk_ok + (int64_t)t * c.B + p;
+  const int64_t qs = (int64_t)c.T * c.B;
+  mk[q * qs] = mk[a * qs];
+}
 
 // Latency mode (small batches, api.cpp): the same paths in the row form of the permutation
 // (lposeidon.h: 16 lanes per path, lane L < 12 holding word L), four paths per wave.  A path is a

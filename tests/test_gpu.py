@@ -451,16 +451,19 @@ def _merkle_top_cases(gc, base_txt, qidx, info, rnd, n_random=40):
     return [json.dumps(d, separators=(",", ":")).encode() for d in cases]
 
 
+@pytest.mark.parametrize("cse", [1, 0])
 @pytest.mark.parametrize("nb", [6, 8, 12])
-def test_gpu_merkle_top_level_mutations_vs_oracle(p2v, nb):
+def test_gpu_merkle_top_level_mutations_vs_oracle(p2v, nb, cse, monkeypatch):
     """Merkle paths near the cap against the oracle's per-path verification
     (Hash/Merkle.hs:27-42): mutations of siblings on nodes shared by several queries of one
     proof, the same change in two queries on one node, bottom values, random changes.  Every
     status and trace word equals the oracle's; the campaign reaches the Merkle failure classes.
-    (Round 3's opt-in path that computed these shared levels once per node was removed in
-    round 4; the campaign now holds k_merkle.)"""
+    cse=1: the shared-node paths (kernels.hip k_merkle_plan / k_merkle_cse / k_merkle_resolve, the
+    default), whose follower checks (A) (B) (C) these mutations hit on both sides of a meeting
+    node; cse=0: k_merkle, one full path per lane.  The batch (> 64 proofs) takes the batch path."""
     import random
     from support import trace_offsets
+    monkeypatch.setenv("P2V_MERKLE_CSE", str(cse))
     O = oracle()
     gc = gen_circuit(nb, 4, 0, 1, 28, 16, 0, 1)
     base = gc.proof(1, 1)
@@ -471,8 +474,40 @@ def test_gpu_merkle_top_level_mutations_vs_oracle(p2v, nb):
     off = trace_offsets(info.num_challenges, info.num_fri_steps, info.num_query_rounds)["query_idx"]
     qidx = [int(x) for x in tr[off: off + info.num_query_rounds]]
     cases = [base] + _merkle_top_cases(gc, base, qidx, info, random.Random(nb))
+    assert len(cases) > 64
     sts, _ = _gpu_vs_oracle(p2v, gc, cases)
     assert {-1, -2} <= set(sts), sorted(set(sts))
+
+
+@pytest.mark.parametrize("nb,lk,mode", [(6, 0, 1), (8, 1, 1), (12, 2, 1)])
+def test_gpu_merkle_shared_nodes_many_proofs(p2v, nb, lk, mode, monkeypatch):
+    """The shared-node Merkle paths over many distinct valid proofs (their query indices meet at
+    every level, including equal leaves in the small step trees) with a corrupted copy of each
+    interleaved: statuses and traces equal the oracle's, and the plain one-path-per-lane kernel
+    (P2V_MERKLE_CSE=0) returns the same words."""
+    gc = gen_circuit(nb, 4, lk, 1, 28, 16, 0, mode)
+    import random
+    rnd = random.Random(77 * nb + lk)
+    cases = []
+    for i in range(40):
+        good = gc.proof(1 + i % 5, 3 + i)
+        cases.append(good)
+        d = json.loads(good)
+        qr = d["proof"]["opening_proof"]["query_round_proofs"]
+        q = rnd.randrange(len(qr))
+        t = rnd.randrange(4)
+        sib = qr[q]["initial_trees_proof"]["evals_proofs"][t][1]["siblings"]
+        if sib:
+            e = sib[rnd.randrange(len(sib))]["elements"]
+            e[0] = (e[0] + 1) % P
+        cases.append(json.dumps(d, separators=(",", ":")).encode())
+    monkeypatch.setenv("P2V_MERKLE_CSE", "1")
+    sts, otr = _gpu_vs_oracle(p2v, gc, cases)
+    assert sts[0::2] == [1] * 40 and -1 in sts[1::2]
+    monkeypatch.setenv("P2V_MERKLE_CSE", "0")
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    res, tr = p2v.BatchVerifier(vk, 0, len(cases)).run(vk.pack_many(cases), trace=True)
+    assert list(res) == sts and np.array_equal(tr, otr)
 
 
 @pytest.mark.parametrize("args,ext", [((6, 4, 0, 1, 28, 16, 0, 1), 0), ((6, 0, 1, 1, 28, 16), 0),
