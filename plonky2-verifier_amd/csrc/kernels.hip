@@ -761,6 +761,9 @@ __device__ __forceinline__ void cse_flag(const DevCircuit& c, int t, int q, int 
   const int at = atomicAdd(c.mfixn, 1);
   if (at < c.mcap) c.mfix[at] = (uint32_t)t << 27 | (uint32_t)q << 22 | (uint32_t)p;
 }
+#ifndef P2V_CSE_INLINE
+#define P2V_CSE_INLINE 0   // 1: a follower failing (A) / (C) re-runs its path in k_merkle_cse, not k_merkle_fix
+#endif
 __device__ __forceinline__ void merkle_chain(const DevCircuit& c) {
   const int lane = threadIdx.x & 63;
   int w = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -824,7 +827,21 @@ __device__ __forceinline__ void merkle_chain(const DevCircuit& c) {
   for (int l = l0; l < depth; l++)   // (C)
 #pragma unroll
     for (int i = 0; i < 4; i++) bad |= ld(c, poff + 4 * l + i, p) != ld(c, oo + 4 * l + i, p);
+#if P2V_CSE_INLINE
+  if (bad) {   // this lane's own data disagrees: its own path to the cap, here (k_merkle_resolve skips it)
+    c.mbadq[((int64_t)t * c.Q + q) * c.B + p] = 1;
+    for (int l = e; l < depth; l++) {
+      uint64_t sib[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) sib[i] = ld(c, poff + 4 * l + i, p);
+      merkle_level(cur, sib, idx & 1u);
+      idx >>= 1;
+    }
+    c.mk_ok[(int64_t)(q * c.T + t) * c.B + p] = cap_ok(c, t, idx, cur, p) ? 1 : 0;
+  }
+#else
   if (bad) cse_flag(c, t, q, p);
+#endif
 }
 #ifndef P2V_CSE_WAVES
 #define P2V_CSE_WAVES 6   // amdgpu_waves_per_eu on k_merkle_cse (80 VGPRs; the spills sit outside the chain loop)
