@@ -70,6 +70,16 @@ def pmc_tag():
     return max(tags) if tags else None
 
 
+def slot_of(kernel):
+    """libp2v's timing slot of a device kernel: the vanishing classes share k_vanish, and the
+    shared-node Merkle kernels (plan / chains / fix / resolve) share k_merkle."""
+    if kernel.startswith("k_vanish") and kernel != "k_vanish_final":
+        return "k_vanish"
+    if kernel.startswith("k_merkle") and kernel != "k_merkle_row":
+        return "k_merkle"
+    return kernel
+
+
 def valu_roofline(kavg, ms_step, B, run_clock_ghz=None):
     """VALU issue utilisation from the latest committed rocprofv3 VALU pass
     (profiles/<tag>_pmc_valu.json, same 4096-proof batch): issue cycles per kernel over its
@@ -83,8 +93,7 @@ def valu_roofline(kavg, ms_step, B, run_clock_ghz=None):
     for k, v in pm.items():
         if k.startswith("_") or not v.get("SQ_INSTS_VALU"):
             continue
-        # the three vanishing kernels share one timing slot (k_vanish) in libp2v
-        kk = "k_vanish" if k.startswith("k_vanish") and k != "k_vanish_final" else k
+        kk = slot_of(k)
         cyc[kk] = cyc.get(kk, 0.0) + VALU_QUAD * (v["SQ_INSTS_VALU"] - (v.get("SQ_ACTIVE_INST_VALU2") or 0.0))
     scale = B / 4096.0   # the PMC pass ran 4096-proof batches
     peak = VALU_SIMDS * VALU_CLOCK_GHZ   # G SIMD-cycles per second
@@ -861,7 +870,8 @@ def main():
         pmc = os.path.join(ROOT, "profiles", f"{tag}_pmc_traffic.json") if tag else ""
         if tag:
             try:
-                traffic_bytes = json.load(open(pmc)).get(dom)
+                pt = json.load(open(pmc))
+                traffic_bytes = sum(v for k, v in pt.items() if not k.startswith("_") and slot_of(k) == dom and isinstance(v, (int, float))) or None
                 if traffic_bytes:
                     traffic_bytes = int(traffic_bytes * B / 4096)   # the PMC passes ran 4096-proof batches
                     traffic = round(traffic_bytes / (kavg[dom] * 1e-3) / 1e9, 2)
@@ -898,6 +908,9 @@ def main():
                          "note": "binding resource: integer VALU issue (Poseidon), valu_issue_frac = valu.issue.step_frac; "
                                  "achieved/peak/frac: the dominant kernel's algorithmic HBM bytes over its launch time"},
             "valu": {"perms_per_proof": ppp, "perm_rate_G": round(value / world * ppp / 1e9, 3),
+                     "perms_note": "perms_per_proof counts every query path in full (the reference's work); the shared-node "
+                                   "Merkle kernels hash each node several queries share once, ~86.6 % of the compressions "
+                                   "(DESIGN.md 5.6), so perm_rate_G is reference-equivalent permutations/s",
                      "issue": valu_roofline(kavg, dt / args.steps * 1e3, B, run_clock)
                      if (real and info.degree_bits == 12 and not args.lookups and not args.ext and not arities) else None},   # the PMC pass's own workload only
             "kernel_ms": {k: round(v, 4) for k, v in kavg.items()},
