@@ -847,33 +847,61 @@ __device__ __forceinline__ void merkle_chain(const DevCircuit& c) {
 #define P2V_CSE_WAVES 6   // amdgpu_waves_per_eu on k_merkle_cse (80 VGPRs; the spills sit outside the chain loop)
 #endif
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P2V_CSE_WAVES))) k_merkle_cse(DevCircuit c) { merkle_chain(c); }
-// The flagged followers, each from its own node at its meeting level to its cap entry (grid-stride
-// over the list; the list length is read once)
-extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle_fix(DevCircuit c) {
+// The flagged followers, each from its own node at its meeting level to its cap entry: a short
+// list (none for honest proofs) on the batch's critical path, so in the row form of the
+// permutation (lposeidon.h: 16 lanes per path, ~8.5 us per dependent compression against ~20 us
+// for one lane), grid-stride over the list rows (the list length is read once)
+extern "C" __global__ void __launch_bounds__(256) k_merkle_fix(DevCircuit c) {
+  __shared__ TLdsAny T;
+  tlds_fill_form(T, 16);
+  __builtin_amdgcn_s_setprio(3);
+  rp::Row R;
+  rp::init(R, threadIdx.x);
+  lp::Row LR;
+  lp::init(LR, T.l, threadIdx.x);
+  const qp::TLds& TQ = T.q;
+  const lp::TLdsL& TL = T.l;
+  (void)LR; (void)TQ; (void)TL;
+  const int L = R.L;
   const int64_t nfix = min((int64_t)*c.mfixn, c.mcap);
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nfix; k += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t rows = (int64_t)gridDim.x * 16;
+  for (int64_t k = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4; k < nfix; k += rows) {   // row-uniform
     const uint32_t id = c.mfix[k];
     const int t = (int)(id >> 27), q = (int)((id >> 22) & 31), p = (int)(id & 0x3FFFFFu);
     const uint32_t pw = c.mplan[((int64_t)tree_class(t) * c.Q + q) * c.B + p];
     uint8_t* mk = c.mk_ok + (int64_t)t * c.B + p;
     const int64_t qs = (int64_t)c.T * c.B;
-    if (!mk[(int64_t)((pw >> 10) & 31) * qs]) { mk[q * qs] = 0; continue; }   // a lower query fails first
+    if (!mk[(int64_t)((pw >> 10) & 31) * qs]) {   // a lower query fails first
+      if (L == 0) mk[q * qs] = 0;
+      continue;
+    }
     const int e = (int)(pw & 15);
     int depth; int64_t poff; uint32_t idx;
     tree_path(c, t, q, p, depth, poff, idx);
-    uint64_t cur[4];
-    const uint64_t* nd = c.mnode + ((int64_t)(t * c.Q + q) * 4) * c.B + p;
-#pragma unroll
-    for (int i = 0; i < 4; i++) cur[i] = nd[(int64_t)i * c.B];
+    uint64_t cur = L < 4 ? c.mnode[((int64_t)(t * c.Q + q) * 4 + L) * c.B + p] : 0;
     idx >>= e;
-    for (int l = e; l < depth; l++) {
-      uint64_t sib[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) sib[i] = ld(c, poff + 4 * l + i, p);
-      merkle_level(cur, sib, idx & 1u);
+    for (int l = e; l < depth; l++) {   // as k_merkle_row
+      const uint64_t sib = L < 8 ? ld(c, poff + 4 * l + (L & 3), p) : 0;
+      const uint64_t c0 = rp::get_word(cur, 0), c1 = rp::get_word(cur, 1), c2 = rp::get_word(cur, 2), c3 = rp::get_word(cur, 3);
+      const uint64_t cb = L == 4 ? c0 : L == 5 ? c1 : L == 6 ? c2 : c3;
+      const bool odd = idx & 1u;
+      const uint64_t x = L < 4 ? (odd ? sib : cur) : L < 8 ? (odd ? cb : sib) : 0;
+      cur = ROW_PERMUTE(x);
       idx >>= 1;
     }
-    mk[q * qs] = cap_ok(c, t, idx, cur, p) ? 1 : 0;
+    bool ok = idx < (uint32_t)c.cap_len;
+    const uint32_t ci = ok ? idx : 0;
+    uint64_t root = 0;
+    if (L < 4) {
+      if (t == 0) root = c.cs_cap[ci * 4 + L];
+      else if (t == 1) root = ld(c, c.wcap + ci * 4 + L, p);
+      else if (t == 2) root = ld(c, c.zcap + ci * 4 + L, p);
+      else if (t == 3) root = ld(c, c.qcap + ci * 4 + L, p);
+      else root = ld(c, c.ccaps + (int64_t)(t - 4) * 4 * c.cap_len + ci * 4 + L, p);
+    }
+    const uint64_t eq = (L >= 4 || root == cur) ? 1 : 0;
+    ok = ok && (rp::get_word(eq, 0) & rp::get_word(eq, 1) & rp::get_word(eq, 2) & rp::get_word(eq, 3));
+    if (L == 0) mk[q * qs] = ok ? 1 : 0;
   }
 }
 extern "C" __global__ void __launch_bounds__(256) k_merkle_resolve(DevCircuit c) {
