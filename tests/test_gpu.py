@@ -893,6 +893,42 @@ def test_gpu_circuit_shape_sweep_vs_oracle(p2v, nb, pis, lk, q, pw):
     assert sts == [1, 1, -3, 0, 0][: len(cases)]
 
 
+@pytest.mark.parametrize("args,ext", [((10, 0, 0, 1, 28, 16), 0), ((13, 9, 0, 1, 28, 16), 0), ((12, 4, 1, 1, 20, 8), 0),
+                                      ((7, 17, 0, 1, 12, 0), 0), ((8, 4, 0, 1, 28, 16, 0, 1, 5, (1, 1, 1, 1)), 5),
+                                      ((6, 4, 0, 1, 28, 16, 0, 1, 7, (3, 2)), 7)])
+def test_gpu_merkle_shared_nodes_shapes(p2v, args, ext, monkeypatch):
+    """The shared-node Merkle paths on the shape sweep and the opt-in conventions, forced onto
+    the batch path (P2V_LAT_MAX=0; small runs otherwise take the row-form k_merkle_row): no public
+    inputs, LDE 2^16 (initial paths of 12 levels, the plan's limit), 20 and 12 queries, odd
+    degree, four arity-2 steps (8 trees), hiding + MinSize + hash_or_noop.  Valid proofs plus
+    copies with one Merkle sibling changed (initial or step tree, any level): statuses and traces
+    equal the oracle's, and P2V_MERKLE_CSE=0 returns the same words."""
+    import random
+    gc = gen_circuit(*args)
+    rnd = random.Random(sum(args[:6]) + ext)
+    base = [gc.proof(1, 1), gc.proof(2, 2)]
+    cases = list(base)
+    for i in range(8):
+        d = json.loads(base[i % 2])
+        qr = d["proof"]["opening_proof"]["query_round_proofs"]
+        q = rnd.randrange(len(qr))
+        trees = [qr[q]["initial_trees_proof"]["evals_proofs"][t][1]["siblings"] for t in range(4)]
+        trees += [st["merkle_proof"]["siblings"] for st in qr[q]["steps"]]
+        sib = trees[rnd.randrange(len(trees))]
+        if sib:
+            e = sib[rnd.randrange(len(sib))]["elements"]
+            e[rnd.randrange(4)] = (e[0] + 1) % P
+        cases.append(json.dumps(d, separators=(",", ":")).encode())
+    monkeypatch.setenv("P2V_LAT_MAX", "0")
+    monkeypatch.setenv("P2V_MERKLE_CSE", "1")
+    sts, otr = _gpu_vs_oracle(p2v, gc, cases, ext=ext)
+    assert sts[:2] == [1, 1]
+    monkeypatch.setenv("P2V_MERKLE_CSE", "0")
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey, ext)
+    res, tr = p2v.BatchVerifier(vk, 0, len(cases)).run(vk.pack_many(cases), trace=True)
+    assert list(res) == sts and np.array_equal(tr, otr)
+
+
 def test_gpu_c_abi_host_example_matches_golden(p2v, tmp_path):
     """examples/p2v_verify.c (plain C over include/p2v.h) on the golden fixtures, one GPU
     and the multi-device entry (--devices 1 shards nothing; the statuses must not change)."""
