@@ -844,7 +844,8 @@ __device__ __forceinline__ void merkle_chain(const DevCircuit& c) {
 #endif
 }
 #ifndef P2V_CSE_WAVES
-#define P2V_CSE_WAVES 6   // amdgpu_waves_per_eu on k_merkle_cse (80 VGPRs; the spills sit outside the chain loop)
+#define P2V_CSE_WAVES 5   // amdgpu_waves_per_eu on k_merkle_cse: 83 VGPRs, no spills; 6 (80 VGPRs, 40 B of spills
+                          // outside the chain loop) measured 0.7-1.4 % slower pipelined (profiles/r05v_cse_waves.txt)
 #endif
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P2V_CSE_WAVES))) k_merkle_cse(DevCircuit c) { merkle_chain(c); }
 // The flagged followers, each from its own node at its meeting level to its cap entry: a short
