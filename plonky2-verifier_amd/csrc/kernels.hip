@@ -844,7 +844,7 @@ __device__ __forceinline__ void merkle_chain(const DevCircuit& c) {
 #endif
 }
 #ifndef P2V_CSE_WAVES
-#define P2V_CSE_WAVES 5   // amdgpu_waves_per_eu on k_merkle_cse: 83 VGPRs, no spills; 6 (80 VGPRs, 40 B of spills
+#define P2V_CSE_WAVES 5   // amdgpu_waves_per_eu on k_merkle_cse: 90 VGPRs, no spills; 6 (80 VGPRs, 40 B of spills
                           // outside the chain loop) measured 0.7-1.4 % slower pipelined (profiles/r05v_cse_waves.txt)
 #endif
 extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(P2V_CSE_WAVES))) k_merkle_cse(DevCircuit c) { merkle_chain(c); }
