@@ -162,7 +162,8 @@ struct p2v_verifier {
                                     // (2048: 2.40 against 2.98 ms serial, 1.084 against 1.077 M proofs/s at two in
                                     // flight; 4096: the same serial, 1.13 against 1.225 M; profiles/r05h_*)
   int lane_min_batch = 16384;       // auto: lane form from this batch size on (env P2V_LANE_MIN)
-  bool merkle_cse = true;           // shared Merkle nodes hashed once (env P2V_MERKLE_CSE=0: one full path per lane)
+  bool merkle_cse = true;
+  bool cse_dirty = false;           // a run enqueued k_merkle_plan but not k_merkle_resolve           // shared Merkle nodes hashed once (env P2V_MERKLE_CSE=0: one full path per lane)
   int lat_max_batch = 64;           // latency mode (row-form Merkle paths, k_fri on its own stream) up to this
                                     // batch size (env P2V_LAT_MAX, measurement)
   bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
@@ -932,6 +933,10 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     // shared nodes once: plan + bucketed chains + followers' statuses (kernels.hip); the chain
     // grid covers every bucket's last partial wave
     const int ncls = 1 + d.S;
+    // k_merkle_resolve zeroes the bucket counters for the next run; a run that stopped between
+    // the plan and the resolve (an error return) leaves them to be zeroed here
+    if (v->cse_dirty) HCK(hipMemsetAsync(v->m_count.p, 0, (size_t)(d.depth0 + 2) * 64, st));
+    v->cse_dirty = true;
     k_merkle_plan<<<(ncls * d.Q * NPB + 15) / 16, 1024, 0, st>>>(d);
     DBG("k_merkle_plan", st);
     const int64_t cse_waves = ((int64_t)d.T * d.Q * d.n + 63) / 64 + d.depth0 + 1;
@@ -941,6 +946,7 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     DBG("k_merkle_fix", st);
     k_merkle_resolve<<<(merkle_units + 3) / 4, 256, 0, st>>>(d);
     DBG("k_merkle_resolve", st);
+    v->cse_dirty = false;
   } else k_merkle<<<(merkle_units + 3) / 4, 256, 0, st>>>(d);
   DBG("k_merkle", st);
   T1(2, st);
