@@ -854,6 +854,8 @@ extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_pe
 // for one lane), grid-stride over the list rows (the list length is read once)
 extern "C" __global__ void __launch_bounds__(256) k_merkle_fix(DevCircuit c) {
   __shared__ TLdsAny T;
+  const int64_t nfix = min((int64_t)*c.mfixn, c.mcap);
+  if ((int64_t)blockIdx.x * 16 >= nfix) return;   // block-uniform: no entry for this block's rows (honest batches: all)
   tlds_fill_form(T, 16);
   __builtin_amdgcn_s_setprio(3);
   rp::Row R;
@@ -864,7 +866,6 @@ extern "C" __global__ void __launch_bounds__(256) k_merkle_fix(DevCircuit c) {
   const lp::TLdsL& TL = T.l;
   (void)LR; (void)TQ; (void)TL;
   const int L = R.L;
-  const int64_t nfix = min((int64_t)*c.mfixn, c.mcap);
   const int64_t rows = (int64_t)gridDim.x * 16;
   for (int64_t k = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4; k < nfix; k += rows) {   // row-uniform
     const uint32_t id = c.mfix[k];
