@@ -34,7 +34,8 @@ def rate(fn, k=2):
     return N / dt
 
 
-for chunk in (4096, 16384):
+CHUNKS = tuple(int(c) for c in os.environ.get("P2V_PROBE_CHUNKS", "4096,16384").split(","))   # 0: auto (about n/8)
+for chunk in CHUNKS:
     for name, arr in (("pageable", host), ("pinned", pinned)):
         if arr is None:
             continue
