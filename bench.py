@@ -124,6 +124,18 @@ def valu_roofline(kavg, ms_step, B, run_clock_ghz=None):
             "note": "all kernels' VALU issue cycles per step over the pipelined step time: the binding resource"}
 
 
+def host_threads(local_world=1, cap=16):
+    """Host threads one rank may use (proof generation, host packing, the CPU baseline): the cores
+    this process may run on -- its affinity mask, capped by the cgroup CPU quota where one is set --
+    shared by the ranks of this node, at most `cap` (on the GPU box the affinity
+    mask shows 256 CPUs and the quota grants 16 cores; 8 ranks x 16 threads oversubscribed them)."""
+    cores = len(os.sched_getaffinity(0))
+    quota = cpu_quota_cores()
+    if quota:
+        cores = min(cores, max(1, int(quota + 0.5)))
+    return max(1, min(cap, cores // max(1, local_world)))
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -667,8 +679,9 @@ def main():
     ap.add_argument("--single-stream", action="store_true", help="P2V_SINGLE_STREAM=1: each workspace on one stream (no side stream)")
     ap.add_argument("--hw-queues", type=int, default=0, help="GPU_MAX_HW_QUEUES for this process (0: the runtime's default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--dist-backend", default="nccl",
-                    help="nccl (= RCCL; the driver's multi-GPU runs) or gloo (rehearsing N ranks on fewer GPUs)")
+    ap.add_argument("--dist-backend", default="gloo",
+                    help="the default process group: gloo (the bench's cross-rank operations are CPU-side barriers and "
+                         "reductions; no data-path collective) or nccl (= RCCL, with a gloo side group for those operations)")
     ap.add_argument("--quick", action="store_true", help="device-resident figure only (no ingest / PCIe / CPU / C5 legs)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 leg (1M proofs sharded over the ranks)")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 leg (65536 lookup-circuit proofs, one GPU)")
@@ -712,11 +725,13 @@ def main():
         saved = os.dup(1)
         os.dup2(2, 1)
         try:
-            dist.init_process_group(args.dist_backend if torch.cuda.is_available() else "gloo")
-            # the bench's only cross-rank operations (barriers, the max-over-ranks time) run on a
-            # gloo side group over CPU tensors: the proofs shard with no data-path collective, so
-            # no RCCL call is needed for the number
-            cpu_grp = dist.new_group(backend="gloo")
+            # the default group is gloo: the proofs shard with no data-path collective, and the bench's
+            # only cross-rank operations (barriers, the max-over-ranks time, the per-rank figures) are
+            # on CPU tensors, so RCCL initialisation is not a failure point of the multi-GPU run
+            # (VERDICT r5 item 2); --dist-backend nccl adds the RCCL group and keeps gloo beside it
+            backend = args.dist_backend if torch.cuda.is_available() else "gloo"
+            dist.init_process_group(backend)
+            cpu_grp = dist.group.WORLD if backend == "gloo" else dist.new_group(backend="gloo")
         finally:
             sys.stdout.flush()
             os.dup2(saved, 1)
@@ -725,8 +740,10 @@ def main():
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     import p2v
+    build = p2v.check_build()   # refuse a libp2v.so built from other sources than this tree
 
-    threads = max(1, min(16, (os.cpu_count() or 8)))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    threads = host_threads(local_world)
     t0 = time.time()
     real = args.circuit == "real"
     arities = tuple(int(a) for a in args.arities.split(",") if a)
@@ -920,6 +937,7 @@ def main():
                              "note": "every timed step's statuses compared with the expected vector on the device, on the "
                                      "launch's stream right after it (p2v_count_mismatches); steps = checks that ran, min over ranks"},
             "per_rank": per_rank,
+            "build": {**build, "host_threads_per_rank": threads, "local_world": local_world},
         }
         if out["valu"]["issue"]:
             out["roofline"]["valu_issue_frac"] = out["valu"]["issue"]["step_frac"]

@@ -40,6 +40,7 @@ import Foreign
 import Foreign.C.String (CString, peekCString)
 import Foreign.C.Types
 import System.IO.Unsafe (unsafePerformIO)
+import System.Mem.StableName (StableName, makeStableName)
 
 import Algebra.Goldilocks (F, fromF, toF)
 import Algebra.GoldilocksExt (FExt, Ext(..), powExt_)
@@ -215,29 +216,62 @@ loadGpuCircuit vkey = withArrayLen (circuitWords vkey) $ \n ws ->
     when (rc /= 0) $ throwLast "p2v_circuit_from_words"
     GpuCircuit <$> (peek out >>= newForeignPtr c_circuit_free)
 
--- | The circuits loaded by 'verifyProof' / 'verifyProofBatch' and the intermediates, keyed by
--- their word encoding, most recent first (at most 'circuitCacheSize').  A repeated call with the
--- same 'VerifierCircuitData' reuses the libp2v circuit handle, and with it the verifier libp2v
--- keeps per circuit and device (p2v_verify_batch's pool, include/p2v.h): no re-decode and no
--- device allocation per call (VERDICT r4 item 2).  A handle dropped from the cache is freed by
--- its finalizer once no call still uses it.
-circuitCache :: IORef [([Word64], GpuCircuit)]
+-- | The circuits loaded by 'verifyProof' / 'verifyProofBatch' and the intermediates, most
+-- recent first (at most 'circuitCacheSize').  A repeated call with the same
+-- 'VerifierCircuitData' reuses the libp2v circuit handle, and with it the verifier libp2v keeps
+-- per circuit and device (p2v_verify_batch's pool, include/p2v.h): no re-decode and no device
+-- allocation per call (VERDICT r4 item 2).  A handle dropped from the cache is freed by its
+-- finalizer once no call still uses it.
+--
+-- Lookup cost (VERDICT r5 item 4).  The hit path is O(1) in the circuit's size: the key is the
+-- 'StableName' of the 'VerifierCircuitData' value the caller passes (pointer identity, the
+-- repeated-call case of a drop-in 'verifyProof'), compared against the few names each entry has
+-- seen; 'circuitWords' is not evaluated.  Another value is first compared by a cheap fingerprint
+-- (the circuit digest, the constants/sigmas cap, the gate and table counts) and only on a
+-- fingerprint match by its full word encoding, which is what decides: the reference does not bind
+-- 'CommonCircuitData' to the digest (src/Types.hs:220-240), so the digest alone is never trusted.
+-- A value whose words match an entry is added to that entry's names.
+data CacheEntry = CacheEntry
+  { ceNames  :: [StableName VerifierCircuitData]   -- values known to have these words (at most circuitNamesMax)
+  , ceFinger :: [Word64]                           -- circuitFingerprint
+  , ceWords  :: [Word64]                           -- circuitWords: the identity that decides
+  , ceCirc   :: GpuCircuit
+  }
+
+circuitCache :: IORef [CacheEntry]
 circuitCache = unsafePerformIO (newIORef [])
 {-# NOINLINE circuitCache #-}
 
-circuitCacheSize :: Int
+circuitCacheSize, circuitNamesMax :: Int
 circuitCacheSize = 4
+circuitNamesMax = 8
+
+-- | O(cap size + #gates + #tables) words, no table entries: a pre-filter, never an identity.
+circuitFingerprint :: VerifierCircuitData -> [Word64]
+circuitFingerprint (MkVerifierCircuitData vonly common) =
+  digest (circuit_digest vonly) ++ cap (constants_sigmas_cap vonly)
+    ++ [ int (length (circuit_gates common)), int (length (circuit_luts common))
+       , int (circuit_num_public_inputs common) ]
 
 cachedGpuCircuit :: VerifierCircuitData -> IO GpuCircuit
 cachedGpuCircuit vkey = do
-  let ws = circuitWords vkey
-  hit <- lookup ws <$> readIORef circuitCache
-  case hit of
-    Just c  -> pure c
-    Nothing -> do
-      c <- loadGpuCircuit vkey
-      atomicModifyIORef' circuitCache (\cs -> (take circuitCacheSize ((ws, c) : filter ((/= ws) . fst) cs), ()))
-      pure c
+  sn <- makeStableName $! vkey
+  cs <- readIORef circuitCache
+  case [e | e <- cs, sn `elem` ceNames e] of
+    (e : _) -> pure (ceCirc e)                     -- hit: pointer identity, O(1) in the circuit
+    [] -> do
+      let fp = circuitFingerprint vkey
+          ws = circuitWords vkey                   -- lazy: forced only on a fingerprint match or a load
+      case [e | e <- cs, ceFinger e == fp, ceWords e == ws] of
+        (e : _) -> do
+          let e' = e { ceNames = take circuitNamesMax (sn : ceNames e) }
+          atomicModifyIORef' circuitCache (\xs -> (e' : filter ((/= ws) . ceWords) xs, ()))
+          pure (ceCirc e)
+        [] -> do
+          c <- loadGpuCircuit vkey
+          let e = CacheEntry [sn] fp ws c
+          atomicModifyIORef' circuitCache (\xs -> (take circuitCacheSize (e : filter ((/= ws) . ceWords) xs), ()))
+          pure c
 
 -- | The same with opt-in plonky2 conventions the reference does not implement (P2V_EXT_* of
 -- include/p2v.h: 1 fri_params arities / MinSize, 2 hiding salts, 4 hash_or_noop leaves).

@@ -132,6 +132,8 @@ struct p2v_verifier {
   size_t max_batch = 0, Bmax = 0;
   DevCircuit dc{};
   std::vector<DevBuf> bufs;
+  size_t in_bytes = 0;              // the host-input staging buffer `in`, allocated by the first run that needs it
+                                    // (device-resident batches never do: a 131 072-proof workspace saves 16.6 GB)
   DevBuf in, soa, chal, leafdig, mk, fbits, qvals, van, vparts, lutre, lutpart, res, trace;
   DevBuf m_plan, m_fol, m_chain, m_count, m_fix, m_badq, m_node;   // shared-node Merkle paths (dev.h mcse)
   DevBuf t_cs, t_kis, t_gkind, t_gpar, t_ggrp, t_gwoff, t_w, t_gs, t_ge, t_lin, t_lout, t_loff, t_llen, t_tw, t_ops, t_vit, t_rin, t_rout, t_roff, t_rch, t_pbase, t_pw;
@@ -162,8 +164,8 @@ struct p2v_verifier {
                                     // (2048: 2.40 against 2.98 ms serial, 1.084 against 1.077 M proofs/s at two in
                                     // flight; 4096: the same serial, 1.13 against 1.225 M; profiles/r05h_*)
   int lane_min_batch = 16384;       // auto: lane form from this batch size on (env P2V_LANE_MIN)
-  bool merkle_cse = true;
-  bool cse_dirty = false;           // a run enqueued k_merkle_plan but not k_merkle_resolve           // shared Merkle nodes hashed once (env P2V_MERKLE_CSE=0: one full path per lane)
+  bool merkle_cse = true;           // shared Merkle nodes hashed once (env P2V_MERKLE_CSE=0: one full path per lane)
+  bool cse_dirty = false;           // a run enqueued k_merkle_plan but not k_merkle_resolve
   int lat_max_batch = 64;           // latency mode (row-form Merkle paths, k_fri on its own stream) up to this
                                     // batch size (env P2V_LAT_MAX, measurement)
   bool single_stream = false;       // env P2V_SINGLE_STREAM=1: no side stream (measurement)
@@ -248,7 +250,6 @@ p2v_circuit::~p2v_circuit() {
 extern "C" {
 
 const char* p2v_last_error_message(void) { return g_err.c_str(); }
-const char* p2v_version(void) { return "p2v 0.1.0 (gfx950)"; }
 const char* p2v_kernel_names(void) { return kKernelNames; }
 
 int p2v_circuit_from_json(const char* common_json, size_t common_len, const char* vkey_json, size_t vkey_len, p2v_circuit** out) {
@@ -418,6 +419,11 @@ int p2v_device_count(void) {
 }
 
 #define HCK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { return fail(P2V_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); } } while (0)
+
+// the staging buffer for batches given in host memory (run from host, JSON / binary ingest)
+static hipError_t input_buf(p2v_verifier* v) {
+  return v->in.p ? hipSuccess : v->in.alloc(v->in_bytes);
+}
 
 void p2v_verifier_free(p2v_verifier* v) {
   if (!v) return;
@@ -624,7 +630,7 @@ int p2v_verifier_create(const p2v_circuit* pc, int device, size_t max_batch, p2v
 #undef UP
   const size_t B = v->Bmax;
   const size_t chw = (size_t)(4 + 7 * d.r + 4 + 2 * d.S + 1 + d.Q + 4);
-  if (e == hipSuccess) e = v->in.alloc((size_t)L.words * v->Bmax * 8);   // whole 64-proof tiles (P2V_FLAG_INPUT_TILED)
+  v->in_bytes = (size_t)L.words * v->Bmax * 8;   // whole 64-proof tiles (P2V_FLAG_INPUT_TILED); allocated on first use
   if (e == hipSuccess && !P2V_PROOF_MAJOR) e = v->soa.alloc((size_t)L.words * B * 8);   // the transposed batch
   if (e == hipSuccess) e = v->chal.alloc(chw * B * 8);
   if (e == hipSuccess) e = v->chal2.alloc(chw * B * 8);
@@ -730,6 +736,7 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
   const uint64_t* src = proofs;
   if (!(flags & P2V_FLAG_INPUT_DEVICE)) {
     const size_t in_words = d.tiled ? p2v_tiled_words(n, (size_t)words) : (size_t)words * n;
+    HCK(input_buf(v));
     HCK(hipMemcpyAsync(v->in.p, proofs, in_words * 8, hipMemcpyHostToDevice, st));
     src = (const uint64_t*)v->in.p;
   }
@@ -942,7 +949,9 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     const int64_t cse_waves = ((int64_t)d.T * d.Q * d.n + 63) / 64 + d.depth0 + 1;
     k_merkle_cse<<<(unsigned)((cse_waves + 3) / 4), 256, 0, st>>>(d);
     DBG("k_merkle_cse", st);
-    k_merkle_fix<<<256, 256, 0, st>>>(d);   // grid-stride over the (usually empty) list
+    // grid-stride over the (usually empty) list: the latency form for up to 16 entries per block,
+    // the lane form beyond (4 waves per SIMD over the whole chip; blocks past the list return at once)
+    k_merkle_fix<<<(unsigned)std::min<int64_t>(1024, std::max<int64_t>(16, (d.mcap + 255) / 256)), 256, 0, st>>>(d);
     DBG("k_merkle_fix", st);
     k_merkle_resolve<<<(merkle_units + 3) / 4, 256, 0, st>>>(d);
     DBG("k_merkle_resolve", st);
@@ -1125,6 +1134,7 @@ static int pack_json_into(p2v_verifier* v, const char* blob, const uint64_t* off
   if (n > v->max_batch) return fail(P2V_E_ARG, "batch larger than max_batch");
   if (n == 0) return P2V_OK;
   HCK(hipSetDevice(v->device));
+  HCK(input_buf(v));
   hipStream_t st = (hipStream_t)stream_;
   const Circuit& C = v->circ->c;
   const int64_t W = C.L.words;
@@ -1217,6 +1227,7 @@ static int pack_bytes_into(p2v_verifier* v, const uint8_t* blob, const uint64_t*
   if (n > v->max_batch) return fail(P2V_E_ARG, "batch larger than max_batch");
   if (n == 0) return P2V_OK;
   HCK(hipSetDevice(v->device));
+  HCK(input_buf(v));
   hipStream_t st = (hipStream_t)stream_;
   const Circuit& C = v->circ->c;
   const int64_t W = C.L.words;

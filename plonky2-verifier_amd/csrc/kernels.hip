@@ -724,7 +724,10 @@ extern "C" __global__ void __launch_bounds__(1024) k_merkle_plan(DevCircuit c) {
     const int64_t pi = ((int64_t)cls * c.Q + q) * c.B + p;
     c.mplan[pi] = (uint32_t)e | (uint32_t)owner << 4 | (uint32_t)(minb == 0) << 9 | (uint32_t)root << 10;
     c.mfol[pi] = fol;
-    for (int tt = 0; tt < ntr; tt++) c.mbadq[((int64_t)(t0 + tt) * c.Q + q) * c.B + p] = 0;
+    for (int tt = 0; tt < ntr; tt++) {
+      c.mbadq[((int64_t)(t0 + tt) * c.Q + q) * c.B + p] = 0;
+      c.mk_ok[(int64_t)(q * c.T + t0 + tt) * c.B + p] = 0;   // written again by its chain, k_merkle_fix or k_merkle_resolve
+    }
   }
   // the wave's lanes of one length: one run of that bucket, tree-major; a work-group's runs are
   // packed in LDS, then one global atomic per (work-group, bucket) places them
@@ -755,11 +758,24 @@ extern "C" __global__ void __launch_bounds__(1024) k_merkle_plan(DevCircuit c) {
     }
   }
 }
-// a follower to re-run from its own node (k_merkle_fix): flag + list entry
+// Set the re-run flag of (t, q, p); true for the one caller that set it first.  A follower can fail
+// two checks, its owner's (B) and its own (A)/(C), so the flag is one bit set by an atomic OR on the
+// flag byte's 32-bit word (the flag array is [T][Q][B], B a multiple of 64: the word is in bounds).
+__device__ __forceinline__ bool cse_flag_once(const DevCircuit& c, int t, int q, int p) {
+  const size_t at = ((size_t)t * c.Q + q) * c.B + p;
+  uint32_t* w = (uint32_t*)(c.mbadq + (at & ~(size_t)3));
+  const uint32_t bit = 1u << (8 * (at & 3));
+  return !(atomicOr(w, bit) & bit);
+}
+// a follower to re-run from its own node (k_merkle_fix): flag + one list entry.  Each (t, q, p) is
+// listed at most once, so the list (capacity T Q B) cannot overflow; the guard below is therefore
+// unreachable, and fails safe: an entry that could not be listed is rejected, never left to a stale
+// status (k_merkle_plan also clears every status byte of the run)
 __device__ __forceinline__ void cse_flag(const DevCircuit& c, int t, int q, int p) {
-  c.mbadq[((int64_t)t * c.Q + q) * c.B + p] = 1;
+  if (!cse_flag_once(c, t, q, p)) return;
   const int at = atomicAdd(c.mfixn, 1);
   if (at < c.mcap) c.mfix[at] = (uint32_t)t << 27 | (uint32_t)q << 22 | (uint32_t)p;
+  else c.mk_ok[(int64_t)(q * c.T + t) * c.B + p] = 0;
 }
 #ifndef P2V_CSE_INLINE
 #define P2V_CSE_INLINE 0   // 1: a follower failing (A) / (C) re-runs its path in k_merkle_cse, not k_merkle_fix
@@ -829,7 +845,7 @@ __device__ __forceinline__ void merkle_chain(const DevCircuit& c) {
     for (int i = 0; i < 4; i++) bad |= ld(c, poff + 4 * l + i, p) != ld(c, oo + 4 * l + i, p);
 #if P2V_CSE_INLINE
   if (bad) {   // this lane's own data disagrees: its own path to the cap, here (k_merkle_resolve skips it)
-    c.mbadq[((int64_t)t * c.Q + q) * c.B + p] = 1;
+    (void)cse_flag_once(c, t, q, p);   // (an entry (B) listed first re-runs the same path in k_merkle_fix)
     for (int l = e; l < depth; l++) {
       uint64_t sib[4];
 #pragma unroll
@@ -852,9 +868,41 @@ extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_pe
 // list (none for honest proofs) on the batch's critical path, so in the row form of the
 // permutation (lposeidon.h: 16 lanes per path, ~8.5 us per dependent compression against ~20 us
 // for one lane), grid-stride over the list rows (the list length is read once)
-extern "C" __global__ void __launch_bounds__(256) k_merkle_fix(DevCircuit c) {
+// One listed follower in the lane form (one lane per entry): a long list (adversarial batches of
+// garbage proofs flag about half of all paths) costs about one k_merkle, not list/rows passes of
+// the latency form
+__device__ __forceinline__ void merkle_fix_lane(const DevCircuit& c, int64_t k) {
+  const uint32_t id = c.mfix[k];
+  const int t = (int)(id >> 27), q = (int)((id >> 22) & 31), p = (int)(id & 0x3FFFFFu);
+  const uint32_t pw = c.mplan[((int64_t)tree_class(t) * c.Q + q) * c.B + p];
+  uint8_t* mk = c.mk_ok + (int64_t)t * c.B + p;
+  const int64_t qs = (int64_t)c.T * c.B;
+  if (!mk[(int64_t)((pw >> 10) & 31) * qs]) { mk[q * qs] = 0; return; }   // a lower query fails first
+  const int e = (int)(pw & 15);
+  int depth; int64_t poff; uint32_t idx;
+  tree_path(c, t, q, p, depth, poff, idx);
+  uint64_t cur[4];
+  const uint64_t* nd = c.mnode + ((int64_t)(t * c.Q + q) * 4) * c.B + p;
+#pragma unroll
+  for (int i = 0; i < 4; i++) cur[i] = nd[(int64_t)i * c.B];
+  idx >>= e;
+  for (int l = e; l < depth; l++) {
+    uint64_t sib[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) sib[i] = ld(c, poff + 4 * l + i, p);
+    merkle_level(cur, sib, idx & 1u);
+    idx >>= 1;
+  }
+  mk[q * qs] = cap_ok(c, t, idx, cur, p) ? 1 : 0;
+}
+extern "C" __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) k_merkle_fix(DevCircuit c) {
   __shared__ TLdsAny T;
   const int64_t nfix = min((int64_t)*c.mfixn, c.mcap);
+  if (nfix > (int64_t)gridDim.x * 16) {   // more entries than latency rows: one lane per entry (grid-uniform)
+    const int64_t lanes = (int64_t)gridDim.x * 256;
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < nfix; k += lanes) merkle_fix_lane(c, k);
+    return;
+  }
   if ((int64_t)blockIdx.x * 16 >= nfix) return;   // block-uniform: no entry for this block's rows (honest batches: all)
   tlds_fill_form(T, 16);
   __builtin_amdgcn_s_setprio(3);

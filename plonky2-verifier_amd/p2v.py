@@ -152,6 +152,27 @@ def lib() -> ctypes.CDLL:
     return L
 
 
+def build_info() -> dict:
+    """The loaded library's version string and source hash (p2v_version, csrc/version.cpp) next to
+    the hash of the sources in this tree (srchash.py), and whether they agree."""
+    import srchash
+    v = lib().p2v_version().decode()
+    built = v.rsplit(" src ", 1)[1] if " src " in v else "unknown"
+    tree = srchash.source_hash(_HERE)
+    return {"version": v, "lib": os.path.abspath(LIB_PATH), "src_hash_built": built, "src_hash_tree": tree,
+            "match": built == tree}
+
+
+def check_build() -> dict:
+    """Refuse a libp2v.so built from other sources than the tree this process runs from
+    (VERDICT r5 item 5).  P2V_LIB builds (A/B measurement variants) are exempt: reported only."""
+    info = build_info()
+    if not info["match"] and not os.environ.get("P2V_LIB"):
+        raise ImportError(f"{info['lib']} was built from sources {info['src_hash_built']}, the tree holds "
+                          f"{info['src_hash_tree']}: rebuild with `make -C {_HERE}`")
+    return info
+
+
 def _check(rc: int) -> None:
     if rc != E_OK:
         raise P2VError(rc, lib().p2v_last_error_message().decode(errors="replace"))

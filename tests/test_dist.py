@@ -176,3 +176,62 @@ def test_bench_per_rank_summary_on_gloo_side_group():
         assert summ["min"] == 2048.0 and summ["max"] == 4096.0
         assert summ["imbalance"] == 0.5
         assert summ["clock_ghz"] == [2.0, 2.1]
+
+
+def test_bench_host_threads_shared_by_local_ranks(monkeypatch):
+    """each rank's host threads are the cores this process may use -- the
+    affinity mask, capped by the cgroup CPU quota -- divided among the node's ranks, at most 16.
+    On the GPU box the mask shows 256 CPUs and the quota grants 16 cores: one rank gets 16
+    threads, each of 8 ranks gets 2 (not 16 each, 128 in all)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(256)))
+    monkeypatch.setattr(bench, "cpu_quota_cores", lambda: 16.0)
+    assert [bench.host_threads(w) for w in (1, 2, 4, 8)] == [16, 8, 4, 2]
+    assert bench.host_threads(32) == 1
+    monkeypatch.setattr(bench, "cpu_quota_cores", lambda: None)   # no quota: the mask
+    assert [bench.host_threads(w) for w in (1, 8)] == [16, 16]
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(8)))
+    assert [bench.host_threads(w) for w in (1, 2, 8, 16)] == [8, 4, 1, 1]
+    monkeypatch.setattr(bench, "cpu_quota_cores", lambda: 2.5)   # a fractional quota rounds to the nearest core
+    assert bench.host_threads(1) == 3
+
+
+def _worker_default_group(rank, world, port, out):
+    """bench.py's process-group setup path: the default group is gloo and is the side group."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    grp = dist.group.WORLD
+    out.put((rank, dist.get_backend(), bench.max_over_ranks(1.0 + rank, world, grp),
+             bench.gather_over_ranks(float(rank), world, grp)))
+    dist.barrier(group=grp)
+    dist.destroy_process_group()
+
+
+def test_bench_default_group_is_gloo():
+    """the bench's default process group is gloo (--dist-backend default), and
+    its cross-rank operations run on it directly -- no RCCL group is created for the number."""
+    import inspect
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    src = inspect.getsource(bench.main)
+    assert 'ap.add_argument("--dist-backend", default="gloo"' in src
+    assert 'dist.group.WORLD if backend == "gloo"' in src
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 4
+    procs = [ctx.Process(target=_worker_default_group, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, backend, mx, ranks in res:
+        assert backend == "gloo" and mx == 4.0 and ranks == [0.0, 1.0, 2.0, 3.0]

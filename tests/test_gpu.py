@@ -510,6 +510,53 @@ def test_gpu_merkle_shared_nodes_many_proofs(p2v, nb, lk, mode, monkeypatch):
     assert list(res) == sts and np.array_equal(tr, otr)
 
 
+def test_gpu_merkle_fix_list_full_batch_of_garbage(p2v, monkeypatch):
+    """a full batch of garbage proofs flags about half of all (tree, query, proof)
+    paths as followers to re-run, many of them twice (their owner's check (B) and their own (A)/(C)).
+    Each path is listed once (kernels.hip cse_flag), the list cannot overflow, and the long list runs
+    in the lane form of k_merkle_fix.  A valid proof with one follower's sibling corrupted above its
+    meeting level (only check (C) sees it) in the last slot, after a run in which every status of
+    the workspace was 1, must still be rejected exactly as the oracle rejects it; every status and
+    trace word equals the plain one-path-per-lane kernel's (P2V_MERKLE_CSE=0)."""
+    from support import trace_offsets
+    O = oracle()
+    gc = gen_circuit(6, 4, 0, 1, 28, 16, 0, 1)
+    base = gc.proof(1, 1)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    info = vk.info
+    st, tr = O.verify_json(gc.common, gc.vkey, base, trace=True)
+    assert st == 1
+    off = trace_offsets(info.num_challenges, info.num_fri_steps, info.num_query_rounds)["query_idx"]
+    qidx = [int(x) for x in tr[off: off + info.num_query_rounds]]
+    d = json.loads(base)
+    qr = d["proof"]["opening_proof"]["query_round_proofs"]
+    dep = len(qr[0]["initial_trees_proof"]["evals_proofs"][0][1]["siblings"])
+    lvl = dep - 1
+    # q shares its node at the top level with a lower query: it meets its owner below that level,
+    # so its top sibling is compared by check (C) only
+    q = next(k for k in range(1, len(qidx)) if any(qidx[h] >> lvl == qidx[k] >> lvl for h in range(k)))
+    e = qr[q]["initial_trees_proof"]["evals_proofs"][2][1]["siblings"][lvl]["elements"]
+    e[1] = (e[1] + 1) % P
+    bad = json.dumps(d, separators=(",", ":")).encode()
+    sb, tb = O.verify_json(gc.common, gc.vkey, bad, trace=True)
+    assert sb == -1
+    n = 4096
+    good = vk.pack_many([base])
+    W = good.shape[1]
+    rng = np.random.default_rng(5)
+    garbage = rng.integers(0, P, size=(n, W), dtype=np.uint64)
+    garbage[-1] = vk.pack_many([bad])[0]
+    monkeypatch.setenv("P2V_MERKLE_CSE", "1")
+    bv = p2v.BatchVerifier(vk, 0, n)
+    res0, _ = bv.run(np.repeat(good, n, axis=0))
+    assert (res0 == 1).all()   # every Merkle status byte of the workspace was 1
+    res, trc = bv.run(garbage, trace=True)
+    assert res[-1] == sb and np.array_equal(trc[-1], tb)
+    monkeypatch.setenv("P2V_MERKLE_CSE", "0")
+    ref, rtr = p2v.BatchVerifier(vk, 0, n).run(garbage, trace=True)
+    assert np.array_equal(res, ref) and np.array_equal(trc, rtr)
+
+
 @pytest.mark.parametrize("args,ext", [((6, 4, 0, 1, 28, 16, 0, 1), 0), ((6, 0, 1, 1, 28, 16), 0),
                                       ((6, 4, 0, 1, 28, 16, 0, 1, 7, (3, 2)), 7)])
 def test_gpu_bytes_ingest_matches_host_reader(p2v, args, ext):

@@ -226,3 +226,25 @@ def test_foreign_imports_are_declared_in_the_header():
 
 if __name__ == "__main__":
     pytest.main([__file__, "-q"])
+
+
+def test_circuit_cache_hit_path_is_constant_time():
+    """the shim's circuit cache is keyed first by the StableName of the
+    VerifierCircuitData value (pointer identity), so a repeated verifyProof with the same value
+    never evaluates circuitWords (O(circuit) words, >130 k for a 2^16-entry table).  Static check
+    of the source: the hit branch, everything before the fingerprint fallback, names no
+    circuitWords; the fallback compares the cheap fingerprint before the full words, and never
+    the digest alone."""
+    hs = _hs()
+    body = hs[hs.index("cachedGpuCircuit vkey = do"):]
+    body = body[: body.index("\n\n")]
+    hit, miss = body.split("let fp = circuitFingerprint vkey", 1)
+    assert "makeStableName $! vkey" in hit and "sn `elem` ceNames e" in hit
+    assert "circuitWords" not in hit
+    assert "ceFinger e == fp, ceWords e == ws" in miss   # fingerprint first, then the identity
+    fp = hs[hs.index("circuitFingerprint (MkVerifierCircuitData"):]
+    fp = fp[: fp.index("\n\n")]
+    assert "circuitWords" not in fp and "circuit_luts" in fp and "lut" not in fp.replace("circuit_luts", "")
+    assert "import System.Mem.StableName (StableName, makeStableName)" in hs
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert "StableName" in doc
