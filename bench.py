@@ -184,6 +184,59 @@ def kernel_bytes_model(info, trace_words):
     }
 
 
+def kernel_bytes_detail(info):
+    """Algorithmic bytes per proof of each device kernel of the default (shared-node Merkle) step,
+    for the per-kernel traffic table.  k_merkle_cse: every sibling, leaf
+    digest, cap word and query index read once (the plain k_merkle's bytes) plus one chain id and
+    one plan / follower word per path; the follower nodes it writes for k_merkle_fix are left out
+    (their number depends on the batch), so the ratio is measured against the smaller figure.
+    k_merkle_plan: the query indices, the plan / follower words, the flag, status and chain-id
+    slots it writes; k_merkle_resolve: one plan word, flag and status per path.  k_merkle_fix has
+    no fixed figure (its list is empty for honest proofs)."""
+    kb = kernel_bytes_model(info, info.trace_words)
+    Q, S = info.num_query_rounds, info.num_fri_steps
+    T, ncls = 4 + S, 1 + S
+    return {
+        "k_phase1": kb["k_phase1"],
+        "k_merkle_plan": Q * 8 + ncls * Q * (4 + 8) + T * Q * (1 + 1 + 4),
+        "k_merkle_cse": kb["k_merkle"] + T * Q * 4 + ncls * Q * (4 + 8),
+        "k_merkle_fix": None,
+        "k_merkle_resolve": T * Q * (4 + 1 + 1),
+        "k_merkle": kb["k_merkle"],
+        "k_fri": kb["k_fri"],
+        "k_vanish": kb["k_vanish"],
+        # without a trace buffer: the path statuses, the FRI check bits, the vanishing results, the status
+        "k_status": T * Q + Q * 4 + (1 + 4 * info.num_challenges) * 8 + 1,
+    }
+
+
+def kernel_traffic_table(pt, info, B):
+    """Every kernel's HBM bytes per launch from the PMC pass (profiles/<tag>_pmc_traffic.json,
+    4096-proof batches, scaled to B) next to its algorithmic bytes per launch and their ratio;
+    the vanishing classes are summed into k_vanish (their model is per proof, all items).  The
+    step's totals compare every kernel's traffic with every kernel's algorithmic bytes."""
+    det = kernel_bytes_detail(info)
+    scale = B / 4096.0
+    rows, van = {}, {}
+    for k, v in pt.items():
+        if k.startswith("_") or not isinstance(v, (int, float)) or not k.startswith("k_") or k in ("k_clock_probe", "k_count_mismatches"):
+            continue
+        if k.startswith("k_vanish") and k != "k_vanish_final":
+            van[k] = v * scale
+            continue
+        alg = det.get(k)
+        rows[k] = {"pmc_bytes": int(v * scale), "algorithmic_bytes": int(alg * B) if alg else None,
+                   "ratio": round(v * scale / (alg * B), 3) if alg else None}
+    if van:
+        tot = sum(van.values())
+        rows["k_vanish"] = {"pmc_bytes": int(tot), "algorithmic_bytes": int(det["k_vanish"] * B),
+                            "ratio": round(tot / (det["k_vanish"] * B), 3), "parts": {k: int(v) for k, v in van.items()}}
+    pmc_tot = sum(r["pmc_bytes"] for r in rows.values())
+    alg_tot = sum(r["algorithmic_bytes"] or 0 for r in rows.values())
+    return {"per_launch": rows, "step_pmc_bytes": pmc_tot, "step_algorithmic_bytes": alg_tot,
+            "step_ratio": round(pmc_tot / alg_tot, 3) if alg_tot else None}
+
+
 def mutate_batch(rows, info, every=16):
     """Corrupt every `every`-th proof of the packed batch in place; returns the expected int8
     statuses.  Alternately (a) the first leaf word of query 0's constants/sigmas tree (initial
@@ -882,12 +935,14 @@ def main():
         # HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
         # (profiles/<tag>_pmc_traffic.json, corrected per MI355X_MICROARCH.md §HBM; the same tag
         # as valu.issue), as GB/s over this run's measured launch time; null if no PMC summary.
-        traffic, traffic_bytes = None, None
+        traffic, traffic_bytes, ktable = None, None, None
         tag = pmc_tag()
         pmc = os.path.join(ROOT, "profiles", f"{tag}_pmc_traffic.json") if tag else ""
         if tag:
             try:
                 pt = json.load(open(pmc))
+                if real and info.degree_bits == 12 and not args.lookups and not args.ext and not arities:
+                    ktable = kernel_traffic_table(pt, info, B)   # the PMC pass's own workload only
                 traffic_bytes = sum(v for k, v in pt.items() if not k.startswith("_") and slot_of(k) == dom and isinstance(v, (int, float))) or None
                 if traffic_bytes:
                     traffic_bytes = int(traffic_bytes * B / 4096)   # the PMC passes ran 4096-proof batches
@@ -921,6 +976,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
                          "traffic_bytes_per_launch": traffic_bytes, "algorithmic_bytes_per_launch": kb[dom] * B,
                          "traffic_source": os.path.relpath(pmc, ROOT) if pmc else None,
+                         "kernels": ktable,
                          "valu_issue_frac": None,
                          "note": "binding resource: integer VALU issue (Poseidon), valu_issue_frac = valu.issue.step_frac; "
                                  "achieved/peak/frac: the dominant kernel's algorithmic HBM bytes over its launch time"},

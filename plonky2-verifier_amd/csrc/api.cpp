@@ -947,7 +947,7 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     k_merkle_plan<<<(ncls * d.Q * NPB + 15) / 16, 1024, 0, st>>>(d);
     DBG("k_merkle_plan", st);
     const int64_t cse_waves = ((int64_t)d.T * d.Q * d.n + 63) / 64 + d.depth0 + 1;
-    k_merkle_cse<<<(unsigned)((cse_waves + 3) / 4), 256, 0, st>>>(d);
+    k_merkle_cse<<<(unsigned)((cse_waves + 31) / 32 * 8), 256, 0, st>>>(d);   // a multiple of 8 blocks (cse_wave: XCD ranges)
     DBG("k_merkle_cse", st);
     // grid-stride over the (usually empty) list: the latency form for up to 16 entries per block,
     // the lane form beyond (4 waves per SIMD over the whole chip; blocks past the list return at once)

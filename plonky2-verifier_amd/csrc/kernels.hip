@@ -75,12 +75,12 @@ __device__ __forceinline__ void leaf_hash_unit(const DevCircuit& c, int unit, in
     // words the rest of the sponge reads: the digest (0..3) after the last block, else the
     // words the next block does not overwrite (nx.. 11); state words 8..11 are 0 in block 0
     int nx = k - 8;
-    p2::permute_dev(st, i == 0, nx <= 0 ? 1 : (nx >= 8 ? 4 : ((7 << (nx >> 2)) & 7)));
+    p2::permute_dev<false>(st, i == 0, nx <= 0 ? 1 : (nx >= 8 ? 4 : ((7 << (nx >> 2)) & 7)));
     if (k > 8) {
 #pragma unroll
       for (int j = 0; j < 8; j++) if (8 + j < k) st[j] = nb[j];
       nx = k - 16;
-      p2::permute_dev(st, false, nx <= 0 ? 1 : (nx >= 8 ? 4 : ((7 << (nx >> 2)) & 7)));
+      p2::permute_dev<false>(st, false, nx <= 0 ? 1 : (nx >= 8 ? 4 : ((7 << (nx >> 2)) & 7)));
     }
   }
   uint64_t* dst = c.leafdig + ((int64_t)(q * c.T + t) * 4) * c.B + p;
@@ -669,6 +669,9 @@ extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCi
 //   k_merkle_fix      the flagged followers (a compact list; none for honest proofs)
 //   k_merkle_resolve  one lane per (tree, query, proof): a follower takes the status of its
 //                     first flagged or root ancestor
+#ifndef P2V_CSE_ORDER
+#define P2V_CSE_ORDER 0   // k_merkle_cse wave order: 0 bucket-major, longest first; 1 tile order merged over the buckets, XCD ranges (round 6, measured slower: see cse_wave)
+#endif
 #define P2V_CSE_CSTRIDE 16   // counters 64 B apart: atomics on one line serialise
 __device__ __forceinline__ void class_shape(const DevCircuit& c, int cls, int& sh, int& depth) {
   sh = 0; depth = c.depth0;
@@ -684,7 +687,13 @@ extern "C" __global__ void __launch_bounds__(1024) k_merkle_plan(DevCircuit c) {
   if (threadIdx.x < (unsigned)nb) hist[threadIdx.x] = 0;
   __syncthreads();
   const bool unit_live = unit < ncls * c.Q * NPB;   // wave-uniform
+  // tile-major (P2V_CSE_ORDER 1): a work-group's units are (tree class, query) pairs of one or two
+  // 64-proof tiles, so the buckets fill tile by tile and k_merkle_cse's merged order follows the tiles
+#if P2V_CSE_ORDER
+  const int cq = unit % (ncls * c.Q), pb = unit / (ncls * c.Q);
+#else
   const int pb = unit % NPB, cq = unit / NPB;
+#endif
   const int q = cq % c.Q, cls = unit_live ? cq / c.Q : 0;
   const int p = pb * 64 + lane;
   const bool live = unit_live && p < c.n;
@@ -780,19 +789,71 @@ __device__ __forceinline__ void cse_flag(const DevCircuit& c, int t, int q, int 
 #ifndef P2V_CSE_INLINE
 #define P2V_CSE_INLINE 0   // 1: a follower failing (A) / (C) re-runs its path in k_merkle_cse, not k_merkle_fix
 #endif
+// Which chains a wave of k_merkle_cse runs: bucket b (the chain length) and wave w of that bucket.
+// P2V_CSE_ORDER 0 (round 5): bucket-major, longest first.  The 64 lanes of a wave are then runs of
+// a few proofs from many 64-proof tiles, and the other proofs of every 128-B line they read sit in
+// other buckets, read long after the line has left the XCD's L2: 6.6x the algorithmic bytes
+// (profiles/r05z_pmc_traffic.json).  P2V_CSE_ORDER 1: the waves of all buckets
+// merged in the order of the plan's tiles (the plan appends tile by tile), so every chain that
+// reads a tile's rows -- all lengths, the owners' and followers' checks -- runs at about the same
+// time, and each XCD takes one contiguous range of that order (blocks i, i + 8, ... share an XCD,
+// MI355X_MICROARCH.md "Workgroup dispatch"), so those reads meet in one L2.  The merge is fraction
+// r of every bucket in turn: waves [r nw_b / R, (r + 1) nw_b / R) of bucket b, longest first within
+// a fraction; fraction r starts at sum_b floor(r nw_b / R), found by bisection.  Scalar work only.
+#define P2V_CSE_LR 12   // R = 4096 fractions
+__device__ __forceinline__ bool cse_wave(const DevCircuit& c, int& b, int64_t& w) {
+  const int nbk = c.depth0 + 1;
+  uint64_t nw[P2V_CSE_MAX_DEPTH + 1];
+  uint64_t total = 0;
+#pragma unroll
+  for (int k = 0; k <= P2V_CSE_MAX_DEPTH; k++) {
+    nw[k] = k < nbk ? ((uint64_t)min((int64_t)c.mcount[k * P2V_CSE_CSTRIDE], c.mcap) + 63) >> 6 : 0;
+    total += nw[k];
+  }
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#if P2V_CSE_ORDER
+  const uint64_t nblk = gridDim.x >> 3;   // the grid is a multiple of 8
+  const uint64_t g = ((uint64_t)(blockIdx.x & 7) * nblk + (blockIdx.x >> 3)) * 4 + wv;
+  if (g >= total) return false;
+  auto start = [&](uint64_t r) {
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k <= P2V_CSE_MAX_DEPTH; k++) s += (r * nw[k]) >> P2V_CSE_LR;
+    return s;
+  };
+  uint64_t r = 0;
+  for (int step = P2V_CSE_LR - 1; step >= 0; step--) {
+    const uint64_t rr = r | (1ull << step);
+    if (start(rr) <= g) r = rr;
+  }
+  uint64_t off = g - start(r);   // < start(r + 1) - start(r): fraction r holds wave g
+  b = -1;
+#pragma unroll
+  for (int k = P2V_CSE_MAX_DEPTH; k >= 0; k--) {
+    const uint64_t lo = (r * nw[k]) >> P2V_CSE_LR, len = (((r + 1) * nw[k]) >> P2V_CSE_LR) - lo;
+    if (b < 0) {
+      if (off < len) { b = k; w = (int64_t)(lo + off); }
+      else off -= len;
+    }
+  }
+  return b >= 0;
+#else
+  int64_t g = (int64_t)blockIdx.x * 4 + wv;
+#pragma unroll
+  for (int k = P2V_CSE_MAX_DEPTH; k >= 0; k--) {   // longest chains first
+    if (g >= 0 && g < (int64_t)nw[k]) { b = k; w = g; }
+    g -= (int64_t)nw[k];
+  }
+  return g < 0;
+#endif
+}
 __device__ __forceinline__ void merkle_chain(const DevCircuit& c) {
   const int lane = threadIdx.x & 63;
-  int w = blockIdx.x * 4 + (threadIdx.x >> 6);
-  int b = c.depth0;   // longest chains first
-  int cnt = 0;
-  for (; b >= 0; b--) {
-    cnt = (int)min((int64_t)c.mcount[b * P2V_CSE_CSTRIDE], c.mcap);
-    const int nw = (cnt + 63) >> 6;
-    if (w < nw) break;
-    w -= nw;
-  }
-  if (b < 0) return;
-  const int slot = w * 64 + lane;
+  int b = -1;
+  int64_t w = 0;
+  if (!cse_wave(c, b, w)) return;
+  const int64_t cnt = min((int64_t)c.mcount[b * P2V_CSE_CSTRIDE], c.mcap);
+  const int64_t slot = w * 64 + lane;
   if (slot >= cnt) return;
   const uint32_t id = c.mchain[(int64_t)b * c.mcap + slot];
   const int t = (int)(id >> 27), q = (int)((id >> 22) & 31), p = (int)(id & 0x3FFFFFu);

@@ -186,6 +186,29 @@ __host__ __device__ constexpr ZhConst make_zh() {
 }
 static __constant__ RcSplit c_rc_split = make_rc_split();
 static __constant__ ZhConst c_zh = make_zh();
+#ifndef P2V_ZH_FOLD
+#define P2V_ZH_FOLD 1   // round 0 of a zh permutation peeled before the round loop, its constant columns folded (below)
+#endif
+// Round 0 of a permutation whose words 8..11 enter as 0 (2-to-1 compression, first sponge block):
+// their S-box outputs z_j are constants (c_zh), so row i of that round's MDS plus round 1's constant
+// is sum_{j<8} M_ij y_j + K_i with K_i = rc[1][i] + sum_{j>=8} M_ij z_j (mod p), whose 32-bit halves
+// start the row's accumulators: 8 MADs per row less (96 per permutation).  Same field elements as
+// Hash/Poseidon.hs:48-52 (fullRound, mdsLayer).
+struct ZrcSplit { uint64_t lo[12], hi[12]; };
+__host__ __device__ constexpr ZrcSplit make_zrc() {
+  ZrcSplit t{};
+  constexpr uint64_t rc[360] = P2V_ALL_ROUND_CONSTANTS_INIT;
+  const ZhConst z = make_zh();
+  for (int i = 0; i < 12; i++) {
+    unsigned __int128 a = rc[12 + i] % gl::P;
+    for (int j = 8; j < 12; j++) a += (unsigned __int128)mds_coeff(i, j) * z.z[j - 8];
+    const uint64_t k = (uint64_t)(a % gl::P);
+    t.lo[i] = k & 0xFFFFFFFFull;
+    t.hi[i] = k >> 32;
+  }
+  return t;
+}
+static __constant__ ZrcSplit c_zrc = make_zrc();
 #endif
 
 // ---------------------------------------------------------------- merged partial rounds
@@ -341,24 +364,25 @@ __device__ __forceinline__ uint64_t reduce_rows(uint64_t al, uint64_t ah) {
   return madm1_co(mask_1(c1), ((uint64_t)rh << 32) | (uint32_t)t, c2);
 #endif
 }
-template <int I, int J>
+template <int I, int J, int E = 12>
 __device__ __forceinline__ void mds_acc(const uint64_t* s, uint64_t& al, uint64_t& ah) {
-  if constexpr (J < 12) {
+  if constexpr (J < E) {
     constexpr uint32_t C = mds_coeff(I, J);
     al = madk<C>((uint32_t)s[J], al);
     ah = madk<C>((uint32_t)(s[J] >> 32), ah);
-    mds_acc<I, J + 1>(s, al, ah);
+    mds_acc<I, J + 1, E>(s, al, ah);
   }
 }
 #if P2V_MDS_BRANCH == 2
-// one row before its (rare) fix-up: r = t + ah_lo 2^32 with the carry-out mask c
-template <int I>
+// one row before its (rare) fix-up: r = t + ah_lo 2^32 with the carry-out mask c.  NW = 8: the
+// row over words 0..7 only (the peeled round 0 of a zh permutation: words 8..11 folded into k)
+template <int I, int NW = 12>
 __device__ __forceinline__ void row_unfixed(const uint64_t* s, const uint64_t* kl, const uint64_t* kh, uint64_t& r, uint64_t& c) {
   using namespace gl::ax;
   constexpr uint32_t C = mds_coeff(I, 0);
   uint64_t al = madk_s<C>((uint32_t)s[0], kl[I]);
   uint64_t ah = madk_s<C>((uint32_t)(s[0] >> 32), kh[I]);
-  mds_acc<I, 1>(s, al, ah);
+  mds_acc<I, 1, NW>(s, al, ah);
   uint64_t c0;
   const uint64_t t = madm1_co((uint32_t)(ah >> 32), al, c0);   // < 2^45: no carry
   const uint32_t rh = add_co((uint32_t)(t >> 32), (uint32_t)ah, c);
@@ -366,14 +390,14 @@ __device__ __forceinline__ void row_unfixed(const uint64_t* s, const uint64_t* k
 }
 // rows I..I+3 with one uniform branch for the group's fix-ups (one basic block per group, so
 // the compiler can batch the group's scalar constant loads)
-template <int I>
+template <int I, int NW = 12>
 __device__ __forceinline__ void mds_group(const uint64_t* s, uint64_t* t, const uint64_t* kl, const uint64_t* kh) {
   using namespace gl::ax;
   uint64_t r0, r1, r2, r3, c0, c1, c2, c3, d;
-  row_unfixed<I>(s, kl, kh, r0, c0);
-  row_unfixed<I + 1>(s, kl, kh, r1, c1);
-  row_unfixed<I + 2>(s, kl, kh, r2, c2);
-  row_unfixed<I + 3>(s, kl, kh, r3, c3);
+  row_unfixed<I, NW>(s, kl, kh, r0, c0);
+  row_unfixed<I + 1, NW>(s, kl, kh, r1, c1);
+  row_unfixed<I + 2, NW>(s, kl, kh, r2, c2);
+  row_unfixed<I + 3, NW>(s, kl, kh, r3, c3);
   if (__builtin_expect((c0 | c1 | c2 | c3) != 0, 0)) {
     r0 = madm1_co(mask_1(c0), r0, d);
     r1 = madm1_co(mask_1(c1), r1, d);
@@ -499,6 +523,17 @@ __device__ __forceinline__ void round_pp(uint64_t* s, uint64_t* t, int r, bool z
   if (g & 4) mds_rows<8, 12>(s, t, kl, kh);
 #endif
 }
+
+#if P2V_MDS_BRANCH == 2 && P2V_ZH_FOLD
+// the peeled round 0 of a zh permutation: s -> t = M sbox(s) + rc[1] with s[8..11] = 0 + rc[0][8..11]
+// never formed (their S-boxes and MDS columns are c_zrc); s[0..7] already hold + rc[0]
+__device__ __forceinline__ void round0_zh(uint64_t* s, uint64_t* t) {
+  sbox_range<0, 8>(s);
+  mds_group<0, 8>(s, t, c_zrc.lo, c_zrc.hi);
+  mds_group<4, 8>(s, t, c_zrc.lo, c_zrc.hi);
+  mds_group<8, 8>(s, t, c_zrc.lo, c_zrc.hi);
+}
+#endif
 
 // ---- merged partial rounds (see PBlock): coefficients are wave-uniform table entries (SGPR
 // operands; gfx950 VOP3 takes no literal, and one SGPR per instruction, so the row's first
@@ -627,6 +662,9 @@ __device__ __forceinline__ void pblock(uint64_t* s, uint64_t* t, const PBlock& B
 //  * rounds alternate between two register sets (s -> t -> s), so no copies are needed at
 //    loop edges; full rounds run as 4 pairs, the 22 partial rounds as merged blocks (PBlock,
 //    P2V_PMERGE; 11 pairs of single rounds with P2V_PMERGE=0).
+// FOLD: compile the peeled zh round 0 (P2V_ZH_FOLD) into this call site; false keeps the round-4
+// code (k_phase1's leaf sponges: the extra path spilled 8 B there, for 168 of its 1 148 permutations)
+template <bool FOLD = true>
 __device__ __forceinline__ void permute_dev(uint64_t s[12], bool zh = false, int gm = 7) {
   uint64_t t[12];
   // keep zh / gm run-time uniform values (uniform branches); as compile-time constants the
@@ -642,14 +680,24 @@ __device__ __forceinline__ void permute_dev(uint64_t s[12], bool zh = false, int
   asm volatile("" : "+s"(rc0));
 #pragma unroll
   for (int i = 0; i < 8; i++) s[i] = add_nc(s[i], rc0[i]);
+  int k0 = 0;
+#if P2V_MDS_BRANCH == 2 && P2V_ZH_FOLD
+  // zh: rounds 0 and 1 peeled before the loop, round 0 over words 0..7 only (c_zrc); the loop body
+  // stays the one generic full-round pair (a second round-0 form inside it spilled, round 5)
+  if constexpr (FOLD) if (zh) {
+    dv::round0_zh(s, t);
+    dv::round_pp<true>(t, s, 1, false, 7);
+    k0 = 1;
+  }
+#endif
   if (!zh) {
 #pragma unroll
     for (int i = 8; i < 12; i++) s[i] = add_nc(s[i], rc0[i]);
   }
 #pragma unroll 1
-  for (int k = 0; k < 4; k++) {   // full-round pairs (0,1) (2,3) (26,27) (28,29)
+  for (int k = k0; k < 4; k++) {   // full-round pairs (0,1) (2,3) (26,27) (28,29)
     const int r = k < 2 ? 2 * k : 22 + 2 * k;
-    dv::round_pp<true>(s, t, r, zh && k == 0, 7);
+    dv::round_pp<true>(s, t, r, zh && k == 0, 7);   // (k == 0 with zh: only when not peeled)
     dv::round_pp<true>(t, s, r + 1, false, k == 3 ? gm : 7);
     if (k == 1) {
 #if P2V_PMERGE == 4
@@ -691,6 +739,7 @@ __device__ __forceinline__ void permute_dev(uint64_t s[12], bool zh = false, int
   for (int i = 0; i < 12; i++) s[i] = gl::canon(s[i]);
 }
 #elif defined(__HIPCC__)
+template <bool FOLD = true>
 __device__ void permute_dev(uint64_t s[12], bool zh = false, int gm = 7);   // device-only
 namespace dv { template <uint32_t C> __device__ uint64_t madk(uint32_t a, uint64_t acc); }
 #endif

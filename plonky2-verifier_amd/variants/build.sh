@@ -10,4 +10,4 @@ mkdir -p variants/build_$NAME
 for t in kernels vanish vanish_poseidon json_pack util; do /opt/rocm/bin/hipcc $F -c -o variants/build_$NAME/$t.o csrc/$t.hip & done
 /opt/rocm/bin/hipcc $F -x hip -c -o variants/build_$NAME/api.o csrc/api.cpp &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o variants/libp2v_$NAME.so variants/build_$NAME/*.o build/circuit.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o variants/libp2v_$NAME.so variants/build_$NAME/*.o build/circuit.o build/version.o

@@ -548,7 +548,7 @@ def test_gpu_merkle_fix_list_full_batch_of_garbage(p2v, monkeypatch):
     garbage[-1] = vk.pack_many([bad])[0]
     monkeypatch.setenv("P2V_MERKLE_CSE", "1")
     bv = p2v.BatchVerifier(vk, 0, n)
-    res0, _ = bv.run(np.repeat(good, n, axis=0))
+    res0 = bv.run(np.repeat(good, n, axis=0))
     assert (res0 == 1).all()   # every Merkle status byte of the workspace was 1
     res, trc = bv.run(garbage, trace=True)
     assert res[-1] == sb and np.array_equal(trc[-1], tb)
