@@ -662,8 +662,9 @@ __device__ __forceinline__ void pblock(uint64_t* s, uint64_t* t, const PBlock& B
 //  * rounds alternate between two register sets (s -> t -> s), so no copies are needed at
 //    loop edges; full rounds run as 4 pairs, the 22 partial rounds as merged blocks (PBlock,
 //    P2V_PMERGE; 11 pairs of single rounds with P2V_PMERGE=0).
-// FOLD: compile the peeled zh round 0 (P2V_ZH_FOLD) into this call site; false keeps the round-4
-// code (k_phase1's leaf sponges: the extra path spilled 8 B there, for 168 of its 1 148 permutations)
+// FOLD: compile the peeled zh round 0 (P2V_ZH_FOLD) into this call site; false leaves it out where zh
+// is never set (the leaf sponge's second block of a trip: with both of its call sites folded,
+// k_phase1 spilled 8 B)
 template <bool FOLD = true>
 __device__ __forceinline__ void permute_dev(uint64_t s[12], bool zh = false, int gm = 7) {
   uint64_t t[12];
@@ -735,8 +736,20 @@ __device__ __forceinline__ void permute_dev(uint64_t s[12], bool zh = false, int
 #endif
     }
   }
+  // canonical outputs for the groups the caller reads (the others are undefined: their last MDS
+  // rows were not formed); a compression's 8 unread words no longer pay ~5 VALU each (round 6)
+  if (gm & 1) {
 #pragma unroll
-  for (int i = 0; i < 12; i++) s[i] = gl::canon(s[i]);
+    for (int i = 0; i < 4; i++) s[i] = gl::canon(s[i]);
+  }
+  if (gm & 2) {
+#pragma unroll
+    for (int i = 4; i < 8; i++) s[i] = gl::canon(s[i]);
+  }
+  if (gm & 4) {
+#pragma unroll
+    for (int i = 8; i < 12; i++) s[i] = gl::canon(s[i]);
+  }
 }
 #elif defined(__HIPCC__)
 template <bool FOLD = true>
