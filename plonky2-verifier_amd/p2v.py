@@ -68,6 +68,7 @@ FLAG_UNIT_FILTERS = 8   # parity mode (tests only): every gate filter / lookup s
 FLAG_INPUT_TILED = 16   # the batch in 64-proof tiles [n/64][words][64] (tile_proofs)
 FLAG_LOOKAHEAD = 32     # the device batch is complete at the call: its transcript may run ahead (include/p2v.h)
 SHAPE_LIMIT = 1 << 20   # public inputs / final-polynomial coefficients a shape variant may hold (include/p2v.h)
+SHAPE_VARIANTS_KEPT = 8   # shape variants a circuit keeps (least recently used evicted)
 
 
 class P2VError(RuntimeError):
@@ -246,12 +247,20 @@ class VerifierCircuitData:
         lengths (p2v_circuit_shape_variant); self when they are the circuit's own."""
         if (num_public_inputs, final_poly_len) == (self.info.num_public_inputs, self.info.final_poly_len):
             return self
-        cache = self.__dict__.setdefault("_variants", {})
+        # the most recently used variants (ADVICE r5 low): a variant's handle owns pooled device
+        # pipelines once it has verified, so proofs of many distinct lengths must not grow device
+        # memory without bound; an evicted variant is freed when its last user drops it
+        from collections import OrderedDict
+        cache = self.__dict__.setdefault("_variants", OrderedDict())
         key = (num_public_inputs, final_poly_len)
-        if key not in cache:
+        if key in cache:
+            cache.move_to_end(key)
+        else:
             h = ctypes.c_void_p()
             _check(lib().p2v_circuit_shape_variant(self._h, num_public_inputs, final_poly_len, ctypes.byref(h)))
             cache[key] = VerifierCircuitData(h.value)
+            while len(cache) > SHAPE_VARIANTS_KEPT:
+                cache.popitem(last=False)
         return cache[key]
 
     def for_proof(self, proof_json: Union[str, bytes]) -> "VerifierCircuitData":

@@ -341,6 +341,28 @@ def test_shape_variant_limits():
     assert vk.shape_variant(0, 0).info.proof_words == vk.info.proof_words - 4 - 8
 
 
+def test_shape_variant_cache_is_bounded():
+    """a circuit keeps at most SHAPE_VARIANTS_KEPT shape variants, least recently
+    used evicted (a variant's handle owns pooled device pipelines once it has verified, so many
+    distinct proof lengths must not grow device memory without bound); an evicted variant's handle
+    is freed once nothing uses it, a kept one is returned again."""
+    import gc as pygc
+    import weakref
+    p2v = p2v_module()
+    gc = gen_circuit(6, 4, 0, 1, 28, 16, 0, 1)
+    vk = p2v.VerifierCircuitData.from_json(gc.common, gc.vkey)
+    K = p2v.SHAPE_VARIANTS_KEPT
+    first = weakref.ref(vk.shape_variant(1, 8))
+    kept = vk.shape_variant(2, 8)
+    for npi in range(3, 3 + K):
+        vk.shape_variant(npi, 8)
+        assert vk.shape_variant(2, 8) is kept          # recently used: stays
+        assert len(vk._variants) <= K
+    pygc.collect()
+    assert first() is None                             # evicted and freed
+    assert (2, 8) in vk._variants and (1, 8) not in vk._variants
+
+
 def test_python_flag_constants_match_the_header():
     """p2v.py's FLAG_* values are the P2V_FLAG_* macros of include/p2v.h (the ABI the ctypes
     mirror passes through), including P2V_FLAG_LOOKAHEAD."""
