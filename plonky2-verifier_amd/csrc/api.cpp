@@ -34,6 +34,12 @@ extern "C" __global__ void k_merkle_row(DevCircuit);
 extern "C" __global__ void k_merkle_plan(DevCircuit);
 extern "C" __global__ void k_merkle_cse(DevCircuit);
 extern "C" __global__ void k_merkle_fix(DevCircuit);
+#ifndef P2V_PLAN_WAVES
+#define P2V_PLAN_WAVES 16   // as kernels.hip
+#endif
+#ifndef P2V_FIX_BLOCKS
+#define P2V_FIX_BLOCKS 256   // k_merkle_fix grid: its blocks wait for free slots beside the other batch's kernels
+#endif
 extern "C" __global__ void k_merkle_resolve(DevCircuit);
 extern "C" __global__ void k_fri(DevCircuit);
 extern "C" __global__ void k_vanish_r2(DevCircuit);
@@ -944,14 +950,15 @@ int p2v_verifier_run(p2v_verifier* v, const uint64_t* proofs, size_t n, int8_t* 
     // the plan and the resolve (an error return) leaves them to be zeroed here
     if (v->cse_dirty) HCK(hipMemsetAsync(v->m_count.p, 0, (size_t)(d.depth0 + 2) * 64, st));
     v->cse_dirty = true;
-    k_merkle_plan<<<(ncls * d.Q * NPB + 15) / 16, 1024, 0, st>>>(d);
+    k_merkle_plan<<<(ncls * d.Q * NPB + P2V_PLAN_WAVES - 1) / P2V_PLAN_WAVES, 64 * P2V_PLAN_WAVES, 0, st>>>(d);
     DBG("k_merkle_plan", st);
     const int64_t cse_waves = ((int64_t)d.T * d.Q * d.n + 63) / 64 + d.depth0 + 1;
     k_merkle_cse<<<(unsigned)((cse_waves + 31) / 32 * 8), 256, 0, st>>>(d);   // a multiple of 8 blocks (cse_wave: XCD ranges)
     DBG("k_merkle_cse", st);
     // grid-stride over the (usually empty) list: the latency form for up to 16 entries per block,
-    // the lane form beyond (4 waves per SIMD over the whole chip; blocks past the list return at once)
-    k_merkle_fix<<<(unsigned)std::min<int64_t>(1024, std::max<int64_t>(16, (d.mcap + 255) / 256)), 256, 0, st>>>(d);
+    // the lane form beyond (one wave per SIMD: a list of every follower, a garbage batch, costs about one
+    // more batch); a larger grid waited ~0.5 ms per launch for free slots beside the other batch (r06e)
+    k_merkle_fix<<<P2V_FIX_BLOCKS, 256, 0, st>>>(d);
     DBG("k_merkle_fix", st);
     k_merkle_resolve<<<(merkle_units + 3) / 4, 256, 0, st>>>(d);
     DBG("k_merkle_resolve", st);

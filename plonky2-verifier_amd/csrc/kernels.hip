@@ -678,10 +678,13 @@ __device__ __forceinline__ void class_shape(const DevCircuit& c, int cls, int& s
   if (cls > 0) { for (int j = 0; j < cls; j++) sh += c.arity[j]; depth = c.step_depth[cls - 1]; }
 }
 __device__ __forceinline__ int tree_class(int t) { return t < 4 ? 0 : t - 3; }
-extern "C" __global__ void __launch_bounds__(1024) k_merkle_plan(DevCircuit c) {
+#ifndef P2V_PLAN_WAVES
+#define P2V_PLAN_WAVES 16   // waves per k_merkle_plan work-group (one global atomic per work-group and bucket)
+#endif
+extern "C" __global__ void __launch_bounds__(64 * P2V_PLAN_WAVES) k_merkle_plan(DevCircuit c) {
   __shared__ int hist[P2V_CSE_MAX_DEPTH + 1], gbase[P2V_CSE_MAX_DEPTH + 1];
   const int lane = threadIdx.x & 63;
-  const int unit = blockIdx.x * 16 + (threadIdx.x >> 6);
+  const int unit = blockIdx.x * P2V_PLAN_WAVES + (threadIdx.x >> 6);
   const int NPB = c.B >> 6, ncls = 1 + c.S;
   const int nb = c.depth0 + 1;
   if (threadIdx.x < (unsigned)nb) hist[threadIdx.x] = 0;

@@ -14,11 +14,11 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/trace -o run -- python3 bench.py --steps 10 --warmup 2 --quick > $OUT/bench_under_trace.json 2> $OUT/trace.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/trace_serial -o run -- python3 bench.py --steps 10 --warmup 2 --quick --inflight 1 > $OUT/bench_under_trace_serial.json 2> $OUT/trace_serial.err
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --quick --inflight 1 > /dev/null 2> $OUT/pmc_fetch.err
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --quick --inflight 1 > /dev/null 2> $OUT/pmc_write.err
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_WAVES SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -T --output-format csv -d $OUT/pmc_valu -o run -- python3 bench.py --steps 3 --warmup 1 --quick --inflight 1 > /dev/null 2> $OUT/pmc_valu.err
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --quick --inflight 1 > /dev/null 2> $OUT/pmc_fetch.err
+timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --quick --inflight 1 > /dev/null 2> $OUT/pmc_write.err
+timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_WAVES SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -T --output-format csv -d $OUT/pmc_valu -o run -- python3 bench.py --steps 3 --warmup 1 --quick --inflight 1 > /dev/null 2> $OUT/pmc_valu.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/c3_trace_serial -o run -- python3 bench.py --steps 10 --warmup 2 --quick --inflight 1 --lookups 2 > $OUT/c3_bench_under_trace_serial.json 2> $OUT/c3_trace_serial.err
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $OUT/c3_pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --quick --inflight 1 --lookups 2 > /dev/null 2> $OUT/c3_pmc_fetch.err
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $OUT/c3_pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --quick --inflight 1 --lookups 2 > /dev/null 2> $OUT/c3_pmc_write.err
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_WAVES SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -T --output-format csv -d $OUT/c3_pmc_valu -o run -- python3 bench.py --steps 3 --warmup 1 --quick --inflight 1 --lookups 2 > /dev/null 2> $OUT/c3_pmc_valu.err
+timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d $OUT/c3_pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --quick --inflight 1 --lookups 2 > /dev/null 2> $OUT/c3_pmc_fetch.err
+timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d $OUT/c3_pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --quick --inflight 1 --lookups 2 > /dev/null 2> $OUT/c3_pmc_write.err
+timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_WAVES SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -T --output-format csv -d $OUT/c3_pmc_valu -o run -- python3 bench.py --steps 3 --warmup 1 --quick --inflight 1 --lookups 2 > /dev/null 2> $OUT/c3_pmc_valu.err
 echo done
