@@ -30,6 +30,15 @@ def p2v():
     return m
 
 
+def test_gpu_library_built_from_this_tree(p2v):
+    """the libp2v.so this process loaded names the hash of the sources it was
+    built from (p2v_version, csrc/version.cpp), and that hash equals srchash.py's recomputation
+    over this tree's csrc/* and include/p2v.h: the binary the GPU tests run is HEAD's."""
+    info = p2v.build_info()
+    print("libp2v", info["version"], "tree", info["src_hash_tree"])
+    assert info["match"], info
+
+
 def _cases(gc):
     from test_oracle import _reject_cases
     out = [(gc.proof(w, s), 1) for w, s in ((1, 1), (2, 2), (1, 9))]

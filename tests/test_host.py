@@ -373,3 +373,29 @@ def test_python_flag_constants_match_the_header():
     assert {"INPUT_DEVICE", "RESULT_DEVICE", "NO_SYNC", "UNIT_FILTERS", "INPUT_TILED", "LOOKAHEAD"} <= set(macros)
     for name, val in macros.items():
         assert getattr(p2v, "FLAG_" + name) == val, name
+
+
+def test_source_hash_covers_the_library_sources(tmp_path):
+    """srchash.py (the hash p2v_version reports and bench.py / smoke() check) covers every
+    top-level file of csrc/ and include/p2v.h, and changes when any of them changes."""
+    import shutil
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "plonky2-verifier_amd"))
+    import srchash
+    pkg = os.path.join(ROOT, "plonky2-verifier_amd")
+    files = srchash.source_files(pkg)
+    assert "csrc/kernels.hip" in files and "csrc/api.cpp" in files and "csrc/version.cpp" in files
+    assert files[-1].replace(os.sep, "/").endswith("include/p2v.h")
+    h = srchash.source_hash(pkg)
+    assert len(h) == 16 and h == srchash.source_hash(pkg)
+    # a copy of the tree with one byte changed in one kernel file hashes differently
+    (tmp_path / "pkg" / "csrc").mkdir(parents=True)
+    (tmp_path / "include").mkdir()
+    for f in os.listdir(os.path.join(pkg, "csrc")):
+        if os.path.isfile(os.path.join(pkg, "csrc", f)):
+            shutil.copy(os.path.join(pkg, "csrc", f), tmp_path / "pkg" / "csrc" / f)
+    shutil.copy(os.path.join(ROOT, "include", "p2v.h"), tmp_path / "include" / "p2v.h")
+    assert srchash.source_hash(str(tmp_path / "pkg")) == h
+    k = tmp_path / "pkg" / "csrc" / "kernels.hip"
+    k.write_bytes(k.read_bytes() + b" ")
+    assert srchash.source_hash(str(tmp_path / "pkg")) != h
