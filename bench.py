@@ -738,6 +738,8 @@ def main():
     ap.add_argument("--quick", action="store_true", help="device-resident figure only (no ingest / PCIe / CPU / C5 legs)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 leg (1M proofs sharded over the ranks)")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 leg (65536 lookup-circuit proofs, one GPU)")
+    ap.add_argument("--no-host-legs", action="store_true",
+                    help="skip the drop-in, ingest, from-host and CPU-baseline legs (device-resident C2 / C5 / C3 only)")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -1001,13 +1003,13 @@ def main():
             out["c5"] = c5
         if c3 is not None:
             out["c3"] = c3
-        if world == 1 and not args.quick:
+        if world == 1 and not args.quick and not args.no_host_legs:
             out["dropin"] = dropin_leg(p2v, gc, proofs, rows, expect, local)
             out["ingest"] = ingest_rate(vk, proofs, threads)
             out["h2d_end_to_end"] = h2d_rate(bvs, rows, B, expect, local=local)
             out["json_end_to_end"] = json_rate(bvs, proofs, B)
             out["bytes_end_to_end"] = bytes_rate(bvs, proofs, B, local=local)
-        if world == 1 and not args.no_cpu_baseline and not args.quick:
+        if world == 1 and not args.no_cpu_baseline and not args.quick and not args.no_host_legs:
             out["cpu_baseline"] = cpu_baseline(gc, proofs, threads)
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -44,6 +44,9 @@ extern "C" __global__ void __launch_bounds__(256) k_transpose(const uint64_t* __
 }
 
 // ------------------------------------------------------------------------ helpers
+#ifndef P2V_LEAF_FOLD
+#define P2V_LEAF_FOLD 1   // the folded zh round 0 (poseidon.h P2V_ZH_FOLD) on each leaf's first block
+#endif
 __device__ __forceinline__ void leaf_hash_unit(const DevCircuit& c, int unit, int lane) {
   const int NPB = c.B >> 6;
   const int pb = unit % NPB, qt = unit / NPB;   // (position, query)-major: costly trees first
@@ -75,7 +78,7 @@ __device__ __forceinline__ void leaf_hash_unit(const DevCircuit& c, int unit, in
     // words the rest of the sponge reads: the digest (0..3) after the last block, else the
     // words the next block does not overwrite (nx.. 11); state words 8..11 are 0 in block 0
     int nx = k - 8;
-    p2::permute_dev<true>(st, i == 0, nx <= 0 ? 1 : (nx >= 8 ? 4 : ((7 << (nx >> 2)) & 7)));
+    p2::permute_dev<P2V_LEAF_FOLD != 0>(st, i == 0, nx <= 0 ? 1 : (nx >= 8 ? 4 : ((7 << (nx >> 2)) & 7)));
     if (k > 8) {
 #pragma unroll
       for (int j = 0; j < 8; j++) if (8 + j < k) st[j] = nb[j];
