@@ -321,7 +321,7 @@ __device__ __forceinline__ void transcript_lane(const DevCircuit& c, int p) {
     const int k = c.num_pis - i;
 #pragma unroll
     for (int j = 0; j < 8; j++) if (j < k) x[j] = ld(c, c.pis + i + j, p);
-    p2::permute_dev(x);
+    p2::permute_dev<false>(x);
   }
   uint64_t pih[4];
 #pragma unroll
@@ -341,7 +341,7 @@ __device__ __forceinline__ void transcript_lane(const DevCircuit& c, int p) {
       for (int k = 0; k < n;) {
         const int start = nbuf == 8 ? 0 : nbuf;
         const int take = (8 - start) < (n - k) ? (8 - start) : (n - k);
-        if (nbuf == 8) { p2::permute_dev(x); nbuf = 0; }   // overwrite mode: the rate part is replaced
+        if (nbuf == 8) { p2::permute_dev<false>(x); nbuf = 0; }   // overwrite mode: the rate part is replaced
 #pragma unroll
         for (int j = 0; j < 8; j++) {   // (loaded after the permutation: no registers held across it)
           const int w = k + j - start;
@@ -356,7 +356,7 @@ __device__ __forceinline__ void transcript_lane(const DevCircuit& c, int p) {
       continue;
     }
     for (int k = 0; k < n; k++) {   // squeeze: output order state[7], state[6], ...
-      if (absorbing || outpos < 0) { p2::permute_dev(x); absorbing = false; outpos = 7; }
+      if (absorbing || outpos < 0) { p2::permute_dev<false>(x); absorbing = false; outpos = 7; }
       uint64_t w;
       switch (outpos) {   // uniform: a switch, not a dynamically indexed (scratch) array
         case 0: w = x[0]; break;
