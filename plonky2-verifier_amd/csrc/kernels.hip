@@ -44,6 +44,9 @@ extern "C" __global__ void __launch_bounds__(256) k_transpose(const uint64_t* __
 }
 
 // ------------------------------------------------------------------------ helpers
+#ifndef P2V_LEAF_PREFETCH
+#define P2V_LEAF_PREFETCH 1   // leaf sponges: each block's words loaded one permutation ahead (0: two blocks per trip, round 5)
+#endif
 #ifndef P2V_LEAF_FOLD
 #define P2V_LEAF_FOLD 1   // the folded zh round 0 (poseidon.h P2V_ZH_FOLD) on each leaf's first block
 #endif
@@ -64,6 +67,26 @@ __device__ __forceinline__ void leaf_hash_unit(const DevCircuit& c, int unit, in
     for (int j = 0; j < 4; j++) if (j < len) st[j] = ld(c, off + j, p);
     len = 0;
   }
+#if P2V_LEAF_PREFETCH
+  // sponge, overwrite mode, no padding.  One 8-word block per trip, its words loaded one
+  // permutation ahead (during the previous block's permutation, into the registers that block has
+  // just been copied out of), so no wave waits for its row at the top of a trip; one permutation
+  // call site (round 6)
+  uint64_t nb[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) nb[j] = j < len ? ld(c, off + j, p) : 0;
+  for (int i = 0; i < len; i += 8) {
+    const int k = len - i;
+#pragma unroll
+    for (int j = 0; j < 8; j++) if (j < k) st[j] = nb[j];
+#pragma unroll
+    for (int j = 0; j < 8; j++) nb[j] = 8 + j < k ? ld(c, off + i + 8 + j, p) : 0;
+    // words the rest of the sponge reads: the digest (0..3) after the last block, else the
+    // words the next block does not overwrite (nx.. 11); state words 8..11 are 0 in block 0
+    const int nx = k - 8;
+    p2::permute_dev<P2V_LEAF_FOLD != 0>(st, i == 0, nx <= 0 ? 1 : (nx >= 8 ? 4 : ((7 << (nx >> 2)) & 7)));
+  }
+#else
   // sponge, overwrite mode, no padding.  Two 8-word blocks per trip, both loaded up front: each
   // lane streams its own proof's row, so the loads of one trip cover a whole 128-B line while
   // it is resident in L2 (one block per load left half of every line to be fetched again after
@@ -86,6 +109,7 @@ __device__ __forceinline__ void leaf_hash_unit(const DevCircuit& c, int unit, in
       p2::permute_dev<false>(st, false, nx <= 0 ? 1 : (nx >= 8 ? 4 : ((7 << (nx >> 2)) & 7)));
     }
   }
+#endif
   uint64_t* dst = c.leafdig + ((int64_t)(q * c.T + t) * 4) * c.B + p;
 #pragma unroll
   for (int i = 0; i < 4; i++) dst[(int64_t)i * c.B] = st[i];
@@ -603,6 +627,21 @@ __device__ __forceinline__ void merkle_level(uint64_t (&cur)[4], const uint64_t 
 #pragma unroll
   for (int i = 0; i < 4; i++) cur[i] = st[i];
 }
+// merkle_level, and the next level's siblings (when `more`, wave-uniform) loaded into sib before
+// the compression runs, so their latency hides behind it
+__device__ __forceinline__ void merkle_level_next(const DevCircuit& c, uint64_t (&cur)[4], uint64_t (&sib)[4], bool odd,
+                                                  bool more, int64_t nxt, int p) {
+  uint64_t st[12];
+#pragma unroll
+  for (int i = 0; i < 4; i++) { st[i] = odd ? sib[i] : cur[i]; st[4 + i] = odd ? cur[i] : sib[i]; st[8 + i] = 0; }
+  if (more) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) sib[i] = ld(c, nxt + i, p);
+  }
+  p2::permute_dev(st, true, 1);
+#pragma unroll
+  for (int i = 0; i < 4; i++) cur[i] = st[i];
+}
 // cap_roots !! (idx >> depth) == the path's root
 __device__ __forceinline__ bool cap_ok(const DevCircuit& c, int t, uint32_t idx, const uint64_t (&cur)[4], int p) {
   bool ok = idx < (uint32_t)c.cap_len;
@@ -672,6 +711,9 @@ extern "C" __global__ void __launch_bounds__(256) P2V_MERKLE_ATTR k_merkle(DevCi
 //   k_merkle_fix      the flagged followers (a compact list; none for honest proofs)
 //   k_merkle_resolve  one lane per (tree, query, proof): a follower takes the status of its
 //                     first flagged or root ancestor
+#ifndef P2V_CSE_PREFETCH
+#define P2V_CSE_PREFETCH 0   // k_merkle_cse: 1 loads each level's siblings one compression ahead (96 VGPRs; measured no gain, profiles/r06l_prefetch.txt)
+#endif
 #ifndef P2V_CSE_ORDER
 #define P2V_CSE_ORDER 0   // k_merkle_cse wave order: 0 bucket-major, longest first; 1 tile order merged over the buckets, XCD ranges (round 6, measured slower: see cse_wave)
 #endif
@@ -871,10 +913,21 @@ __device__ __forceinline__ void merkle_chain(const DevCircuit& c) {
   tree_path(c, t, q, p, depth, poff, idx);
   uint64_t cur[4];
   load_leafdig(c, t, q, p, cur);
+#if P2V_CSE_PREFETCH
+  // each level's siblings are loaded one compression ahead, into the registers the compression
+  // has just consumed, so no wave waits for them at the top of a level
+  uint64_t sib[4];
+  if (e > 0) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) sib[i] = ld(c, poff + i, p);
+  }
+#endif
   for (int l = 0; l < e; l++) {
+#if !P2V_CSE_PREFETCH
     uint64_t sib[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) sib[i] = ld(c, poff + 4 * l + i, p);
+#endif
     const int f = (int)((fol >> (5 * l)) & 31);
     if (f != 31) {   // (B): the follower meeting this path here holds this node as its sibling
       const int64_t fo = poff + (int64_t)(f - q) * c.qstride + 4 * l;
@@ -883,7 +936,11 @@ __device__ __forceinline__ void merkle_chain(const DevCircuit& c) {
       for (int i = 0; i < 4; i++) bad |= ld(c, fo + i, p) != cur[i];
       if (bad) cse_flag(c, t, f, p);
     }
+#if P2V_CSE_PREFETCH
+    merkle_level_next(c, cur, sib, idx & 1u, l + 1 < e, poff + 4 * (l + 1), p);
+#else
     merkle_level(cur, sib, idx & 1u);
+#endif
     idx >>= 1;
   }
   if (e == depth) {
