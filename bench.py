@@ -662,6 +662,8 @@ C3_PROOFS = 65536   # BASELINE.json configs[2]
 C3_CHUNK = 16384
 C3_PASSES = 3   # timed passes over the 65 536 proofs (one pass is ~56 ms: a clock dip after the workload's
                 # generation on the host read 0.66 M once, profiles/r04q_vanish_items_merge.txt)
+C3_WARM = 4     # untimed passes first: with 2, the first bench process on a fresh box read ~0.97 M
+                # against ~1.20 M for every later one, whichever library ran (profiles/r06t_c3_ab_rev.txt)
 
 
 def c3_leg(p2v, args, threads, dev, local, streams):
@@ -682,10 +684,10 @@ def c3_leg(p2v, args, threads, dev, local, streams):
     d_expect = torch.from_numpy(expect).to(dev)
     gen_s = time.time() - t0
     out = c5_leg(p2v, vk, info, d_proofs, d_expect, args.batch, 1, local, dev, None, streams, True,
-                 total=C3_PROOFS, chunk=C3_CHUNK, steps=C3_PASSES, warm=2,
+                 total=C3_PROOFS, chunk=C3_CHUNK, steps=C3_PASSES, warm=C3_WARM,
                  note="BASELINE configs[2]: 65536 proofs of the real circuit with LookupGate/LookupTableGate (256 + 65536-entry "
                       "tables, live lookup argument), device-resident, launches of 16384, two in flight, statuses checked on the device; "
-                      "timed over 3 passes after 2 untimed ones ('proofs' counts all three)")
+                      f"timed over {C3_PASSES} passes after {C3_WARM} untimed ones ('proofs' counts all three)")
     bv = p2v.BatchVerifier(vk, local, args.batch)
     res = torch.empty(args.batch, dtype=torch.int8, device=dev)
     kt = {}

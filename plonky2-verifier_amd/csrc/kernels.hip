@@ -156,7 +156,8 @@ __device__ __forceinline__ E horner_strided(const DevCircuit& c, int64_t off, in
 
 // the row form's permutation: lposeidon.h (round 5: LDS exchange, merged partial blocks; 8.1-8.6 us
 // per dependent permutation against 11.7-12.3 us for the DPP form of rposeidon.h,
-// profiles/r05e_lrow_chain.txt); P2V_ROW_LAT=0 rebuilds the DPP form
+// profiles/r05e_lrow_chain.txt; round 6: chain rows on the idle lanes, 6.6-6.8 us,
+// profiles/r06p_row_par.txt); P2V_ROW_LAT=0 rebuilds the DPP form
 #ifndef P2V_ROW_LAT
 #define P2V_ROW_LAT 1
 #endif

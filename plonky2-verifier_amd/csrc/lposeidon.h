@@ -13,6 +13,8 @@
 //   * the 22 partial rounds as the merged blocks of poseidon.h (PBlock, D = 4,4,4,4,4,2): with
 //     the whole state in every lane, each lane runs the block's S-box chain itself (y_1..y_D
 //     through the chain rows) and then its own output row: one exchange per block instead of D;
+//     round 6 (pblock_par) moves the chain rows' dot products onto the idle lanes 12-14, off the
+//     serial path: 8.2-8.5 -> 6.6-6.8 us per dependent permutation (profiles/r06p_row_par.txt);
 //   * the S-box multiply and the row reductions as single inline-asm statements (the compiler
 //     pads an s_nop after every inline-asm statement with an SGPR output, an issue slot of the
 //     lone wave each time); the MADs are plain C with coefficients in registers (no asm, no
@@ -204,12 +206,70 @@ __device__ __forceinline__ uint64_t pblock(uint64_t x, const p2::PBlock& B, cons
   return D == 4 ? red_wide(al, ah) : red_small(al, ah);
 }
 
+// Round 6: the same block with its chain rows on the row's idle lanes.  pblock above evaluates
+// chain row k (a 12-term dot product over s') between S-box k and S-box k + 1, so three dot
+// products sit on the lone wave's serial path per block.  None of them depends on the chain
+// except through its y terms.  Here every lane of the row evaluates one row's s'-part in the same
+// dot product: lanes 0..11 their output rows, lanes 12, 13, 14 chain rows 1, 2, 3.  Then the
+// chain is, per S-box, one reduction in every lane, a broadcast of the chain lane's value to its
+// row (DPP row_newbcast) and the S-box.  Each lane adds y_m times its own row's coefficient:
+//   output row L: H_D[L][m] (cf[12 + m - 2]) for m < D, M[L][0] for m = D;
+//   chain row 2 (lane 13): M[0][0] for y_2;  chain row 3 (lane 14): H_3[0][2] (cf[12]) for y_2,
+//   M[0][0] for y_3.
+// A lane's sum is read only at the step where it is complete (lane 12 at S-box 2, 13 at 3, 14 at
+// 4, the output rows after the block).  That sum has the same non-negative terms as pblock's, so
+// the same reduction bounds hold.  The other lanes' reductions of partial sums are never read.
+// Lane 15 repeats lane 13's row and is never read.
+#ifndef P2V_ROW_PAR
+#define P2V_ROW_PAR 1   // 0: pblock (round 5), the chain rows between the S-boxes
+#endif
+// lane S of each 16-lane row, to the whole row (DPP row_newbcast: a VALU move, no LDS round trip)
+template <int S>
+__device__ __forceinline__ uint64_t row_bcast(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x150 + S, 0xf, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x150 + S, 0xf, 0xf, false);
+  return (uint64_t)hi << 32 | lo;
+}
+template <int D>
+__device__ __forceinline__ uint64_t pblock_par(uint64_t x, const p2::PBlock& B, const Row& R, const TLdsL& T, uint32_t c0) {
+  uint64_t s[12];
+  exchange(x, R.xb, R.L, s);
+  const int L = R.L;
+  const uint32_t* cf = L < 12 ? B.cf[2 + L] : (L == 12 ? T.m[0] : B.cf[L == 14 ? 1 : 0]);
+  const int di = L < 12 ? 4 + L : (L == 15 ? 1 : L - 12);
+  uint64_t al = B.dlo[di], ah = B.dhi[di];
+  const uint4 hk = *(const uint4*)(cf + 12);   // H coefficients (zero where the row has none)
+  const uint32_t m00 = T.m[0][0];
+  s[0] = sbox(s[0]);   // y_1, word 0 of s'
+  dot12(cf, s, al, ah);
+  uint64_t y = sbox(row_bcast<12>(red_small(al, ah)));   // y_2
+  {
+    const uint32_t k = D == 2 ? c0 : (L == 13 ? m00 : hk.x);
+    al = madr((uint32_t)y, k, al); ah = madr((uint32_t)(y >> 32), k, ah);
+  }
+  if constexpr (D >= 3) {
+    y = sbox(row_bcast<13>(red_small(al, ah)));   // y_3
+    const uint32_t k = D == 3 ? c0 : (L == 14 ? m00 : hk.y);
+    al = madr((uint32_t)y, k, al); ah = madr((uint32_t)(y >> 32), k, ah);
+  }
+  if constexpr (D >= 4) {
+    y = sbox(row_bcast<14>(red_small(al, ah)));   // y_4
+    al = madr((uint32_t)y, c0, al); ah = madr((uint32_t)(y >> 32), c0, ah);
+  }
+  return D == 4 ? red_wide(al, ah) : red_small(al, ah);
+}
+
 // the row's permutation; x = this lane's word (inputs < 2^64, outputs canonical)
 __device__ __forceinline__ uint64_t permute(uint64_t x, const Row& R, const TLdsL& T) {
   x = p2::add_nc(x, T.rc0[R.Lc]);
 #pragma unroll 1
   for (int r = 0; r < 4; r++) x = full_round(x, r, R, T);
-#if P2V_PMERGE == 4
+#if P2V_PMERGE == 4 && P2V_ROW_PAR
+  const uint32_t c0 = T.m[R.Lc][0];   // M[L][0]: the output row's y_D coefficient
+#pragma unroll 1
+  for (int b = 0; b < 5; b++) x = pblock_par<4>(x, T.pm[b], R, T, c0);
+  x = pblock_par<2>(x, T.pm[5], R, T, c0);
+#elif P2V_PMERGE == 4
 #pragma unroll 1
   for (int b = 0; b < 5; b++) x = pblock<4>(x, T.pm[b], R, T);
   x = pblock<2>(x, T.pm[5], R, T);
