@@ -14,7 +14,8 @@
 //     the whole state in every lane, each lane runs the block's S-box chain itself (y_1..y_D
 //     through the chain rows) and then its own output row: one exchange per block instead of D;
 //     round 6 (pblock_par) moves the chain rows' dot products onto the idle lanes 12-14, off the
-//     serial path: 8.2-8.5 -> 6.6-6.8 us per dependent permutation (profiles/r06p_row_par.txt);
+//     serial path: 8.2-8.5 -> 6.6-6.8 us per dependent permutation (profiles/r06p_row_par.txt),
+//     and splits their S-boxes' x^3 / x^4 over lane pairs (sbox_u): 6.2-6.4 us (r06u_row_sbox2.txt);
 //   * the S-box multiply and the row reductions as single inline-asm statements (the compiler
 //     pads an s_nop after every inline-asm statement with an SGPR output, an issue slot of the
 //     lone wave each time); the MADs are plain C with coefficients in registers (no asm, no
@@ -230,6 +231,28 @@ __device__ __forceinline__ uint64_t row_bcast(uint64_t v) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x150 + S, 0xf, 0xf, false);
   return (uint64_t)hi << 32 | lo;
 }
+// x^7 of a value every lane of the row holds (the partial rounds' S-box inputs): x^3 and x^4 are
+// independent, so even lanes form x^3 = x x^2 and odd lanes x^4 = x^2 x^2 in one multiply, swap
+// them with their neighbour (DPP quad_perm [1,0,3,2]) and multiply: three multiplies on the
+// serial path instead of four.  Bit-identical to sbox(): mul_lat's result is a function of the
+// 128-bit product alone (the cross terms a0 b1 + a1 b0 enter as one sum), so x^3 x^4 and x^4 x^3
+// agree.
+#ifndef P2V_ROW_SBOX2
+#define P2V_ROW_SBOX2 1   // 0: sbox() for the uniform S-box inputs too
+#endif
+__device__ __forceinline__ uint64_t sbox_u(uint64_t x, int L) {
+#if P2V_ROW_SBOX2
+  const uint64_t x2 = mul_lat(x, x);
+  const uint64_t h = mul_lat((L & 1) ? x2 : x, x2);
+  constexpr int kSwap = 1 | (0 << 2) | (3 << 4) | (2 << 6);
+  const uint32_t olo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)h, kSwap, 0xf, 0xf, false);
+  const uint32_t ohi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(h >> 32), kSwap, 0xf, 0xf, false);
+  return mul_lat(h, (uint64_t)ohi << 32 | olo);
+#else
+  (void)L;
+  return sbox(x);
+#endif
+}
 template <int D>
 __device__ __forceinline__ uint64_t pblock_par(uint64_t x, const p2::PBlock& B, const Row& R, const TLdsL& T, uint32_t c0) {
   uint64_t s[12];
@@ -240,20 +263,20 @@ __device__ __forceinline__ uint64_t pblock_par(uint64_t x, const p2::PBlock& B, 
   uint64_t al = B.dlo[di], ah = B.dhi[di];
   const uint4 hk = *(const uint4*)(cf + 12);   // H coefficients (zero where the row has none)
   const uint32_t m00 = T.m[0][0];
-  s[0] = sbox(s[0]);   // y_1, word 0 of s'
+  s[0] = sbox_u(s[0], L);   // y_1, word 0 of s'
   dot12(cf, s, al, ah);
-  uint64_t y = sbox(row_bcast<12>(red_small(al, ah)));   // y_2
+  uint64_t y = sbox_u(row_bcast<12>(red_small(al, ah)), L);   // y_2
   {
     const uint32_t k = D == 2 ? c0 : (L == 13 ? m00 : hk.x);
     al = madr((uint32_t)y, k, al); ah = madr((uint32_t)(y >> 32), k, ah);
   }
   if constexpr (D >= 3) {
-    y = sbox(row_bcast<13>(red_small(al, ah)));   // y_3
+    y = sbox_u(row_bcast<13>(red_small(al, ah)), L);   // y_3
     const uint32_t k = D == 3 ? c0 : (L == 14 ? m00 : hk.y);
     al = madr((uint32_t)y, k, al); ah = madr((uint32_t)(y >> 32), k, ah);
   }
   if constexpr (D >= 4) {
-    y = sbox(row_bcast<14>(red_small(al, ah)));   // y_4
+    y = sbox_u(row_bcast<14>(red_small(al, ah)), L);   // y_4
     al = madr((uint32_t)y, c0, al); ah = madr((uint32_t)(y >> 32), c0, ah);
   }
   return D == 4 ? red_wide(al, ah) : red_small(al, ah);
