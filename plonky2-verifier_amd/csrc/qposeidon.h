@@ -180,11 +180,29 @@ __device__ __forceinline__ void chain_part(const uint64_t (&X)[4][3], const p2::
     ah += (w >> 32) * c;
   }
 }
+// The chain's S-boxes (inputs the same in all four lanes of the quad): x^3 on lanes 0, 2 and x^4 on
+// lanes 1, 3, swapped and multiplied (lp::sbox_u, round 6): three multiplies per lane instead of
+// four, bit-identical (P2V_QUAD_SBOX2=0: sbox_q)
+#ifndef P2V_QUAD_SBOX2
+#define P2V_QUAD_SBOX2 1
+#endif
+__device__ __forceinline__ uint64_t sbox_qu(uint64_t x, int t) {
+#if P2V_QUAD_SBOX2 && P2V_QUAD_SBOX
+  return lp::sbox_u(x, t);
+#else
+  (void)t;
+  return sbox_q(x);
+#endif
+}
 template <int D>
 __device__ __forceinline__ void qblock(uint64_t x[3], int t, const p2::PBlock& B, const QBlock& Q) {
   // y1 = sbox(word 0) from lane 0; s' = the state with y1 in word 0
   uint64_t y[D + 1];
+#if P2V_QUAD_SBOX2 && P2V_QUAD_SBOX
+  y[1] = sbox_qu(bcast64(x[0], 0), t);
+#else
   y[1] = bcast64(sbox_q(x[0]), 0);
+#endif
   x[0] = t == 0 ? y[1] : x[0];
   uint64_t X[4][3];
 #pragma unroll
@@ -196,11 +214,11 @@ __device__ __forceinline__ void qblock(uint64_t x[3], int t, const p2::PBlock& B
   chain_part<1>(X, B, pl[1], ph[1]);
   pl[1] = bcast64(pl[1], 0); ph[1] = bcast64(ph[1], 0);
   if constexpr (D >= 3) { chain_part<2>(X, B, pl[2], ph[2]); pl[2] = bcast64(pl[2], 0); ph[2] = bcast64(ph[2], 0); }
-  y[2] = sbox_q(p2::mds_reduce(pl[1], ph[1]));
+  y[2] = sbox_qu(p2::mds_reduce(pl[1], ph[1]), t);
   if constexpr (D >= 4) { chain_part<3>(X, B, pl[3], ph[3]); pl[3] = bcast64(pl[3], 0); ph[3] = bcast64(ph[3], 0); }
   if constexpr (D >= 3) {
     constexpr uint32_t c = p2::mds_coeff(0, 0);
-    y[3] = sbox_q(p2::mds_reduce(pl[2] + (uint64_t)(uint32_t)y[2] * c, ph[2] + (y[2] >> 32) * c));
+    y[3] = sbox_qu(p2::mds_reduce(pl[2] + (uint64_t)(uint32_t)y[2] * c, ph[2] + (y[2] >> 32) * c), t);
   }
   // per-lane output-row coefficients, one row at a time (row m + 1's loads overlap row m), the
   // first row's before the last S-box: 17 VGPRs in flight instead of 51
@@ -217,7 +235,7 @@ __device__ __forceinline__ void qblock(uint64_t x[3], int t, const p2::PBlock& B
     const uint64_t al = pl[3] + (uint64_t)(uint32_t)y[2] * h2 + (uint64_t)(uint32_t)y[3] * c;
     const uint64_t ah = ph[3] + (y[2] >> 32) * h2 + (y[3] >> 32) * c;
     load_row(0);
-    y[4] = sbox_q(p2::mds_reduce(al, ah));
+    y[4] = sbox_qu(p2::mds_reduce(al, ah), t);
   } else {
     load_row(0);
   }
