@@ -662,8 +662,10 @@ C3_PROOFS = 65536   # BASELINE.json configs[2]
 C3_CHUNK = 16384
 C3_PASSES = 3   # timed passes over the 65 536 proofs (one pass is ~56 ms: a clock dip after the workload's
                 # generation on the host read 0.66 M once, profiles/r04q_vanish_items_merge.txt)
-C3_WARM = 4     # untimed passes first: with 2, the first bench process on a fresh box read ~0.97 M
-                # against ~1.20 M for every later one, whichever library ran (profiles/r06t_c3_ab_rev.txt)
+C3_WARM = 4     # untimed passes first.  The first bench process on a fresh box reads ~0.97 M against
+                # ~1.20 M for every later one, whichever library runs, with 2 warm passes and with 4:
+                # host-side time inside the bracket, not device time (profiles/r06t_c3_ab_rev.txt,
+                # r06z2_first_process.txt)
 
 
 def c3_leg(p2v, args, threads, dev, local, streams):
